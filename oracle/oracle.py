@@ -1,0 +1,240 @@
+"""ctypes front-end for the CPU oracle (test infrastructure only).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this module.  The product path (beast_amd/) never does.
+
+`liboracle.so` is the clean-room C restatement of Beast's zlib + pmd framing
+(see bzo.h); `_ref/libzref.so` is the reference's vendored zlib 1.3.1,
+compiled in place from /root/reference by oracle/Makefile (present only where
+it could be built).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+_REF = None
+
+# zlib::error values (include/boost/beast/zlib/error.hpp:48-138)
+ERRORS = {
+    0: "ok", 1: "need_buffers", 2: "end_of_stream", 3: "need_dict", 4: "stream_error",
+    5: "invalid_block_type", 6: "invalid_stored_length", 7: "too_many_symbols",
+    8: "invalid_code_lengths", 9: "invalid_bit_length_repeat", 10: "missing_eob",
+    11: "invalid_literal_length", 12: "invalid_distance_code", 13: "invalid_distance",
+    14: "over_subscribed_length", 15: "incomplete_length_set", 16: "general",
+}
+ERROR_CODES = {v: k for k, v in ERRORS.items()}
+
+FLUSH = {"none": 0, "block": 1, "partial": 2, "sync": 3, "full": 4, "finish": 5, "trees": 6}
+STRATEGY = {"normal": 0, "filtered": 1, "huffman": 2, "rle": 3, "fixed": 4}
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = ctypes.CDLL(path)
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        L.bzo_inflate_new.restype = ctypes.c_void_p
+        L.bzo_deflate_new.restype = ctypes.c_void_p
+        L.bzo_inflate_free.argtypes = [ctypes.c_void_p]
+        L.bzo_deflate_free.argtypes = [ctypes.c_void_p]
+        L.bzo_inflate_reset.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.bzo_inflate_write.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.bzo_deflate_reset_params.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 4
+        L.bzo_deflate_reset.argtypes = [ctypes.c_void_p]
+        L.bzo_deflate_write.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.bzo_deflate_upper_bound.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+        L.bzo_deflate_upper_bound.restype = ctypes.c_size_t
+        L.bzo_deflate_upper_bound_free.argtypes = [ctypes.c_size_t]
+        L.bzo_deflate_upper_bound_free.restype = ctypes.c_size_t
+        L.bzo_pmd_deflate_msg.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                          ctypes.c_void_p, ctypes.c_size_t]
+        L.bzo_pmd_deflate_msg.restype = ctypes.c_long
+        L.bzo_pmd_inflate_msg.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                          ctypes.c_void_p, ctypes.c_size_t,
+                                          ctypes.POINTER(ctypes.c_size_t), ctypes.c_int]
+        vp = ctypes.c_void_p
+        L.bzo_pmd_deflate_batch.argtypes = [ctypes.c_int] * 4 + [vp] * 3 + [ctypes.c_uint32] + [vp] * 5 + [ctypes.c_int]
+        L.bzo_pmd_inflate_batch.argtypes = [ctypes.c_int, ctypes.c_int] + [vp] * 3 + [ctypes.c_uint32] + [vp] * 5 + [ctypes.c_int]
+        _LIB = L
+    return _LIB
+
+
+def ref():
+    """The reference's own zlib 1.3.1 (None when it could not be built)."""
+    global _REF
+    if _REF is None:
+        path = os.path.join(HERE, "_ref", "libzref.so")
+        if not os.path.exists(path):
+            return None
+        R = ctypes.CDLL(path)
+        R.zref_deflate.argtypes = [ctypes.c_int] * 5 + [ctypes.c_void_p, ctypes.c_ulong,
+                                                       ctypes.c_void_p, ctypes.c_ulong]
+        R.zref_deflate.restype = ctypes.c_long
+        R.zref_inflate.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_ulong, ctypes.c_void_p,
+                                   ctypes.c_ulong, ctypes.POINTER(ctypes.c_int)]
+        R.zref_inflate.restype = ctypes.c_long
+        _REF = R
+    return _REF
+
+
+class ZParams(ctypes.Structure):
+    _fields_ = [("next_in", ctypes.c_void_p), ("avail_in", ctypes.c_size_t),
+                ("total_in", ctypes.c_size_t), ("next_out", ctypes.c_void_p),
+                ("avail_out", ctypes.c_size_t), ("total_out", ctypes.c_size_t),
+                ("data_type", ctypes.c_int)]
+
+
+def _buf(b: bytes):
+    return ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p) if b else None
+
+
+def upper_bound(n: int) -> int:
+    """deflate_upper_bound (zlib/deflate_stream.hpp:402-410)."""
+    return lib().bzo_deflate_upper_bound_free(n)
+
+
+def pmd_deflate(data: bytes, level=6, wbits=15, mem_level=4, strategy=0) -> bytes:
+    L = lib()
+    z = L.bzo_deflate_new()
+    try:
+        r = L.bzo_deflate_reset_params(z, level, wbits, mem_level, strategy)
+        if r:
+            raise ValueError("invalid deflate parameters")
+        cap = upper_bound(len(data)) + 64
+        out = ctypes.create_string_buffer(cap)
+        src = ctypes.create_string_buffer(data, len(data)) if data else None
+        n = L.bzo_pmd_deflate_msg(z, src, len(data), out, cap)
+        if n < 0:
+            raise RuntimeError(f"deflate failed: {ERRORS.get(-n, -n)}")
+        return out.raw[:n]
+    finally:
+        L.bzo_deflate_free(z)
+
+
+def pmd_inflate(payload: bytes, cap: int = 1 << 20, wbits=15, raw=False):
+    """Returns (status, output bytes)."""
+    L = lib()
+    z = L.bzo_inflate_new()
+    try:
+        if L.bzo_inflate_reset(z, wbits):
+            raise ValueError("windowBits out of range")
+        out = ctypes.create_string_buffer(max(cap, 1))
+        got = ctypes.c_size_t(0)
+        src = ctypes.create_string_buffer(payload, len(payload)) if payload else None
+        st = L.bzo_pmd_inflate_msg(z, src, len(payload), out, cap, ctypes.byref(got), 1 if raw else 0)
+        return st, out.raw[:got.value]
+    finally:
+        L.bzo_inflate_free(z)
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def deflate_batch(data: np.ndarray, off: np.ndarray, lens: np.ndarray, level=6, wbits=15,
+                  mem_level=4, strategy=0, threads=1):
+    """Batch pmd deflate; returns (out, out_off, out_len, status)."""
+    n = len(lens)
+    cap = np.array([upper_bound(int(x)) + 16 for x in lens], dtype=np.uint32)
+    out_off = np.zeros(n, dtype=np.uint64)
+    if n:
+        out_off[1:] = np.cumsum(cap[:-1].astype(np.uint64))
+    out = np.zeros(int(cap.astype(np.uint64).sum()) + 1, dtype=np.uint8)
+    out_len = np.zeros(n, dtype=np.uint32)
+    status = np.zeros(n, dtype=np.int32)
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    lib().bzo_pmd_deflate_batch(level, wbits, mem_level, strategy, _p(data), _p(off), _p(lens),
+                                n, _p(out), _p(out_off), _p(cap), _p(out_len), _p(status), threads)
+    return out, out_off, out_len, status
+
+
+def inflate_batch(data: np.ndarray, off: np.ndarray, lens: np.ndarray, out_cap: np.ndarray,
+                  wbits=15, raw=False, threads=1):
+    """Batch pmd inflate; returns (out, out_off, out_len, status)."""
+    n = len(lens)
+    out_cap = np.ascontiguousarray(out_cap, dtype=np.uint32)
+    out_off = np.zeros(n, dtype=np.uint64)
+    if n:
+        out_off[1:] = np.cumsum(out_cap[:-1].astype(np.uint64))
+    out = np.zeros(int(out_cap.astype(np.uint64).sum()) + 1, dtype=np.uint8)
+    out_len = np.zeros(n, dtype=np.uint32)
+    status = np.zeros(n, dtype=np.int32)
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    lib().bzo_pmd_inflate_batch(wbits, 1 if raw else 0, _p(data), _p(off), _p(lens), n, _p(out),
+                                _p(out_off), _p(out_cap), _p(out_len), _p(status), threads)
+    return out, out_off, out_len, status
+
+
+def ref_pmd_deflate(data: bytes, level=6, wbits=15, mem_level=4, strategy=0, mode=0):
+    R = ref()
+    if R is None:
+        return None
+    cap = upper_bound(len(data)) + 64
+    out = ctypes.create_string_buffer(cap)
+    src = ctypes.create_string_buffer(data, len(data)) if data else None
+    n = R.zref_deflate(level, wbits, mem_level, strategy, mode, src, len(data), out, cap)
+    if n < 0:
+        raise RuntimeError("reference zlib deflate failed")
+    return out.raw[:n]
+
+
+class Inflater:
+    """Streaming zlib::inflate_stream restatement (inflate_stream.hpp:63-213)."""
+
+    def __init__(self, wbits=15):
+        self.L = lib()
+        self.z = self.L.bzo_inflate_new()
+        self.reset(wbits)
+
+    def reset(self, wbits=15):
+        r = self.L.bzo_inflate_reset(self.z, wbits)
+        if r:
+            raise ValueError("windowBits out of range")
+
+    def write(self, zs: ZParams, flush: str) -> int:
+        return self.L.bzo_inflate_write(self.z, ctypes.byref(zs), FLUSH[flush])
+
+    def __del__(self):
+        try:
+            self.L.bzo_inflate_free(self.z)
+        except Exception:
+            pass
+
+
+class Deflater:
+    """Streaming zlib::deflate_stream restatement (deflate_stream.hpp:59-369)."""
+
+    def __init__(self, level=6, wbits=15, mem_level=9, strategy=0):
+        self.L = lib()
+        self.z = self.L.bzo_deflate_new()
+        if self.L.bzo_deflate_reset_params(self.z, level, wbits, mem_level, strategy):
+            raise ValueError("invalid deflate parameters")
+
+    def reset(self):
+        self.L.bzo_deflate_reset(self.z)
+
+    def write(self, zs: ZParams, flush: str) -> int:
+        return self.L.bzo_deflate_write(self.z, ctypes.byref(zs), FLUSH[flush])
+
+    def __del__(self):
+        try:
+            self.L.bzo_deflate_free(self.z)
+        except Exception:
+            pass
