@@ -1,0 +1,69 @@
+"""Builds the in-tree HIP library `beast_amd/libbeast_pmd.so` for gfx950.
+
+hipcc compiles each translation unit under csrc/ (in parallel) and links one
+shared library exporting the C ABI of include/beast_pmd.h.  The library is
+built in-tree so it travels to the GPU box with the repository snapshot.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+BUILD = os.path.join(HERE, "_build")
+LIB = os.path.join(HERE, "libbeast_pmd.so")
+SYNTH = os.path.join(HERE, "libbpmd_synth.so")
+ARCH = os.environ.get("BPMD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
+            "-munsafe-fp-atomics"]
+
+
+def _sources():
+    return sorted(f for f in os.listdir(CSRC) if f.endswith(".hip"))
+
+
+def _headers_mtime():
+    hs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    hs.append(os.path.join(HERE, "..", "include", "beast_pmd.h"))
+    return max(os.path.getmtime(h) for h in hs if os.path.exists(h))
+
+
+def _compile(src: str, hmt: float) -> str:
+    obj = os.path.join(BUILD, src.replace(".hip", ".o"))
+    s = os.path.join(CSRC, src)
+    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(s), hmt):
+        return obj
+    cmd = [HIPCC, *CXXFLAGS, "-c", s, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
+    return obj
+
+
+def build(verbose: bool = False) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    hmt = _headers_mtime()
+    srcs = _sources()
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        objs = list(ex.map(lambda s: _compile(s, hmt), srcs))
+    newest = max(os.path.getmtime(o) for o in objs)
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < newest:
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr}")
+    synth_src = os.path.join(CSRC, "synth.c")
+    if not os.path.exists(SYNTH) or os.path.getmtime(SYNTH) < os.path.getmtime(synth_src):
+        subprocess.run(["gcc", "-O2", "-fPIC", "-shared", "-o", SYNTH, synth_src, "-lm"], check=True)
+    if verbose:
+        print("built", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(verbose=True)
+    sys.exit(0)

@@ -1,0 +1,57 @@
+// pmd_capi.hip -- extern "C" entry points declared in include/beast_pmd.h.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <mutex>
+
+#include "../../include/beast_pmd.h"
+
+extern "C" int bpmd_internal_init_fixed(void);
+extern "C" int bpmd_internal_inflate_v1(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                        uint32_t n, uint8_t* out, const uint64_t* out_off,
+                                        const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
+                                        uint32_t raw, hipStream_t stream);
+
+namespace {
+std::mutex g_init_mu;
+int g_init_device = -1;   // device whose symbols are initialised
+}
+
+extern "C" const char* bpmd_version(void) { return "beast_pmd 0.1 (gfx950)"; }
+
+extern "C" int bpmd_init(void)
+{
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess) return BPMD_R_NO_DEVICE;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return BPMD_R_NO_DEVICE;
+    std::lock_guard<std::mutex> lk(g_init_mu);
+    if (g_init_device == dev) return BPMD_R_OK;
+    if (bpmd_internal_init_fixed() != 0) return BPMD_R_HIP_ERROR;
+    g_init_device = dev;
+    return BPMD_R_OK;
+}
+
+extern "C" size_t bpmd_deflate_upper_bound(size_t n)
+{
+    // zlib/deflate_stream.hpp:402-410
+    return n + ((n + 7) >> 3) + ((n + 63) >> 6) + 11;
+}
+
+extern "C" int bpmd_inflate_batch(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_off,
+                                  const uint32_t* d_in_len, uint32_t n_msgs, uint8_t* d_out,
+                                  const uint64_t* d_out_off, const uint32_t* d_out_cap,
+                                  uint32_t* d_out_len, int32_t* d_status, void* stream)
+{
+    if (!cfg) return BPMD_R_INVALID_ARGUMENT;
+    // inflate_stream.ipp:57-61: windowBits outside 8..15 throws domain_error
+    if (cfg->window_bits < 8 || cfg->window_bits > 15) return BPMD_R_DOMAIN_ERROR;
+    if (n_msgs == 0) return BPMD_R_OK;
+    if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_cap || !d_out_len || !d_status)
+        return BPMD_R_INVALID_ARGUMENT;
+    int r = bpmd_init();
+    if (r) return r;
+    int e = bpmd_internal_inflate_v1(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
+                                     d_status, (cfg->flags & BPMD_F_RAW) ? 1u : 0u, (hipStream_t)stream);
+    return e ? BPMD_R_HIP_ERROR : BPMD_R_OK;
+}

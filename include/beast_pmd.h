@@ -1,0 +1,105 @@
+/*
+ * beast_pmd.h -- C ABI of the MI355X permessage-deflate engine.
+ *
+ * Drop-in boundary for Boost.Beast's WebSocket permessage-deflate path.  In
+ * Beast the only caller of the codec is websocket::stream<..., true> through
+ * impl_base<true> (include/boost/beast/websocket/detail/impl_base.hpp:85-202),
+ * which calls exactly:
+ *     zo.reset(level, wbits, memLevel, Strategy::normal)   impl_base.hpp:295-307
+ *     zo.write(zs, Flush::{none,block,sync}, ec)            impl_base.hpp:104-141
+ *     zo.reset()                                            impl_base.hpp:156-166
+ *     zi.reset(wbits)  zi.write(zs, Flush::sync, ec)        impl_base.hpp:168-190, 295-305
+ * Each entry point below names the reference interface it replaces.
+ *
+ * Conventions: plain pointers and sizes only.  All functions are noexcept and
+ * return 0 on success or a negative bpmd_result; per-message outcomes are
+ * Beast's zlib::error values (include/boost/beast/zlib/error.hpp:48-138) in
+ * the status array.  Device pointers refer to memory of the current HIP
+ * device; `stream` is a hipStream_t (0 = default stream).  Batch calls are
+ * asynchronous on `stream` and never allocate.
+ */
+#ifndef BEAST_PMD_H
+#define BEAST_PMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* zlib::error (zlib/error.hpp:48-138) */
+enum bpmd_status {
+    BPMD_OK = 0,
+    BPMD_NEED_BUFFERS = 1,
+    BPMD_END_OF_STREAM = 2,
+    BPMD_NEED_DICT = 3,
+    BPMD_STREAM_ERROR = 4,
+    BPMD_INVALID_BLOCK_TYPE = 5,
+    BPMD_INVALID_STORED_LENGTH = 6,
+    BPMD_TOO_MANY_SYMBOLS = 7,
+    BPMD_INVALID_CODE_LENGTHS = 8,
+    BPMD_INVALID_BIT_LENGTH_REPEAT = 9,
+    BPMD_MISSING_EOB = 10,
+    BPMD_INVALID_LITERAL_LENGTH = 11,
+    BPMD_INVALID_DISTANCE_CODE = 12,
+    BPMD_INVALID_DISTANCE = 13,
+    BPMD_OVER_SUBSCRIBED_LENGTH = 14,
+    BPMD_INCOMPLETE_LENGTH_SET = 15,
+    BPMD_GENERAL = 16
+};
+
+/* call-level results (negative) */
+enum bpmd_result {
+    BPMD_R_OK = 0,
+    BPMD_R_INVALID_ARGUMENT = -1,   /* reference throws std::invalid_argument */
+    BPMD_R_DOMAIN_ERROR = -2,       /* reference throws std::domain_error */
+    BPMD_R_HIP_ERROR = -3,
+    BPMD_R_NO_DEVICE = -4
+};
+
+/* zlib::Strategy (zlib/zlib.hpp:209-246) */
+enum bpmd_strategy {
+    BPMD_STRATEGY_NORMAL = 0, BPMD_STRATEGY_FILTERED = 1, BPMD_STRATEGY_HUFFMAN = 2,
+    BPMD_STRATEGY_RLE = 3, BPMD_STRATEGY_FIXED = 4
+};
+
+/* flags */
+#define BPMD_F_RAW 1u   /* inflate: plain inflate_stream::write() semantics, no 00 00 FF FF tail */
+
+/* Codec configuration: the subset of websocket::permessage_deflate
+ * (websocket/option.hpp:34-67) that reaches the codec after negotiation
+ * (impl_base.hpp:277-309). */
+typedef struct bpmd_cfg {
+    int level;        /* compLevel 0..9 (-1 = 6) */
+    int window_bits;  /* 9..15 for deflate (8 is bumped to 9), 8..15 for inflate */
+    int mem_level;    /* 1..9 */
+    int strategy;     /* bpmd_strategy */
+    uint32_t flags;
+} bpmd_cfg;
+
+/* Library / device bring-up.  Idempotent.  Returns BPMD_R_NO_DEVICE when no
+ * HIP device is visible (the engine has no CPU fallback). */
+int bpmd_init(void);
+/* Library version string. */
+const char* bpmd_version(void);
+
+/* Batched inflate of independent permessage-deflate payloads (replaces one
+ * zi.reset(wbits) + zi.write(zs, Flush::sync) + inflate_with_eb() sequence
+ * per message: impl_base.hpp:168-190, websocket/impl/read.hpp:1284-1356).
+ *   d_in + d_in_off[i], d_in_len[i]   payload i without the 00 00 FF FF tail
+ *   d_out + d_out_off[i], d_out_cap[i] output slot i
+ *   d_out_len[i]  bytes produced;  d_status[i]  zlib::error of message i
+ *                 (need_buffers = output exceeded d_out_cap[i]) */
+int bpmd_inflate_batch(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_off,
+                       const uint32_t* d_in_len, uint32_t n_msgs, uint8_t* d_out,
+                       const uint64_t* d_out_off, const uint32_t* d_out_cap,
+                       uint32_t* d_out_len, int32_t* d_status, void* stream);
+
+/* deflate_upper_bound (zlib/deflate_stream.hpp:402-410): size a d_out slot. */
+size_t bpmd_deflate_upper_bound(size_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
