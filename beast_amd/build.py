@@ -32,27 +32,32 @@ def _headers_mtime():
     return max(os.path.getmtime(h) for h in hs if os.path.exists(h))
 
 
-def _compile(src: str, hmt: float) -> str:
-    obj = os.path.join(BUILD, src.replace(".hip", ".o"))
+def _compile(src: str, hmt: float, bdir: str = BUILD, extra=()) -> str:
+    obj = os.path.join(bdir, src.replace(".hip", ".o"))
     s = os.path.join(CSRC, src)
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(s), hmt):
         return obj
-    cmd = [HIPCC, *CXXFLAGS, "-c", s, "-o", obj]
+    cmd = [HIPCC, *CXXFLAGS, *extra, "-c", s, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
     return obj
 
 
-def build(verbose: bool = False) -> str:
-    os.makedirs(BUILD, exist_ok=True)
+def build(verbose: bool = False, variant: str = "") -> str:
+    """variant "" = the product library; "prof" = diagnostic build with
+    per-phase cycle counters (libbeast_pmd_prof.so, never loaded by default)."""
+    bdir = BUILD + (f"_{variant}" if variant else "")
+    lib = LIB.replace(".so", f"_{variant}.so") if variant else LIB
+    extra = ("-DBPMD_PROF",) if variant == "prof" else ()
+    os.makedirs(bdir, exist_ok=True)
     hmt = _headers_mtime()
     srcs = _sources()
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-        objs = list(ex.map(lambda s: _compile(s, hmt), srcs))
+        objs = list(ex.map(lambda s: _compile(s, hmt, bdir, extra), srcs))
     newest = max(os.path.getmtime(o) for o in objs)
-    if not os.path.exists(LIB) or os.path.getmtime(LIB) < newest:
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs]
+    if not os.path.exists(lib) or os.path.getmtime(lib) < newest:
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *objs]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr}")
@@ -60,10 +65,10 @@ def build(verbose: bool = False) -> str:
     if not os.path.exists(SYNTH) or os.path.getmtime(SYNTH) < os.path.getmtime(synth_src):
         subprocess.run(["gcc", "-O2", "-fPIC", "-shared", "-o", SYNTH, synth_src, "-lm"], check=True)
     if verbose:
-        print("built", LIB)
-    return LIB
+        print("built", lib)
+    return lib
 
 
 if __name__ == "__main__":
-    build(verbose=True)
+    build(verbose=True, variant=sys.argv[1] if len(sys.argv) > 1 else "")
     sys.exit(0)

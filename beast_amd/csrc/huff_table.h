@@ -44,7 +44,8 @@ BPMD_HD inline bool slot_is_link(uint16_t s) { return slot_kind(s) == K_SPECIAL 
 // `lens` values are 0..15; `sorted` needs room for ncodes entries.
 template <typename LenT, typename SlotT>
 BPMD_HD inline int build_table(int type, const LenT* lens, unsigned ncodes, SlotT* tab,
-                               unsigned* root_io, unsigned* used, uint16_t* sorted)
+                               unsigned* root_io, unsigned* used, uint16_t* sorted,
+                               unsigned* min_len = nullptr)
 {
     uint16_t cnt[16], first[16];
     for (unsigned i = 0; i < 16; ++i) cnt[i] = 0;
@@ -59,10 +60,12 @@ BPMD_HD inline int build_table(int type, const LenT* lens, unsigned ncodes, Slot
         tab[1] = slot(K_SPECIAL, 1, V_INVALID);
         *root_io = 1;
         *used = 2;
+        if (min_len) *min_len = 1;
         return 0;
     }
     unsigned lo = 1;
     while (lo < hi && cnt[lo] == 0) ++lo;
+    if (min_len) *min_len = lo;
     if (root < lo) root = lo;
 
     int avail = 1;

@@ -7,7 +7,7 @@
 #include "../../include/beast_pmd.h"
 
 extern "C" int bpmd_internal_init_fixed(void);
-extern "C" int bpmd_internal_inflate_v1(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+extern "C" int bpmd_internal_inflate(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                         uint32_t n, uint8_t* out, const uint64_t* out_off,
                                         const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
                                         uint32_t raw, hipStream_t stream);
@@ -51,7 +51,7 @@ extern "C" int bpmd_inflate_batch(const bpmd_cfg* cfg, const uint8_t* d_in, cons
         return BPMD_R_INVALID_ARGUMENT;
     int r = bpmd_init();
     if (r) return r;
-    int e = bpmd_internal_inflate_v1(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
+    int e = bpmd_internal_inflate(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
                                      d_status, (cfg->flags & BPMD_F_RAW) ? 1u : 0u, (hipStream_t)stream);
     return e ? BPMD_R_HIP_ERROR : BPMD_R_OK;
 }

@@ -1,0 +1,80 @@
+// pmd_diag.hip -- self-check entry point for tests: builds decode tables for
+// many code-length vectors with both the wave-cooperative builder
+// (huff_wave.h) and the serial restatement of the reference's inflate_table
+// (huff_table.h) so a test can compare them slot for slot on the device.
+#include "pmd_common.h"
+#include "huff_table.h"
+#include "huff_wave.h"
+
+namespace bpmd {
+
+struct alignas(16) DiagLds {
+    WaveTableScratch ts;
+    uint8_t lens[320];
+    uint16_t sorted[320];
+    uint16_t tab_wave[kEnough];
+    uint16_t tab_serial[kEnough];
+};
+
+__global__ void __launch_bounds__(64)
+diag_tables_kernel(const uint8_t* lens_all, const uint32_t* n_all, const int32_t* type_all, uint32_t count,
+                   uint16_t* out_wave, uint16_t* out_serial, int32_t* meta)
+{
+    __shared__ DiagLds L;
+    const unsigned lane = lane_id();
+    for (uint32_t c = blockIdx.x; c < count; c += gridDim.x) {
+        const uint32_t n = n_all[c];
+        const int type = type_all[c];
+        for (unsigned i = lane; i < 320; i += 64) L.lens[i] = lens_all[c * 320 + i];
+        for (unsigned i = lane; i < kEnough; i += 64) { L.tab_wave[i] = 0xffff; L.tab_serial[i] = 0xffff; }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        const unsigned req = type == BUILD_CODES ? 7 : type == BUILD_LENS ? 9 : 6;
+        unsigned root = 0, used = 0, lmin = 0;
+        int r;
+        if (type == BUILD_CODES) r = build_table_wave<BUILD_CODES>(L.lens, n, L.tab_wave, req, L.ts, root, used, lmin);
+        else if (type == BUILD_LENS) r = build_table_wave<BUILD_LENS>(L.lens, n, L.tab_wave, req, L.ts, root, used, lmin);
+        else r = build_table_wave<BUILD_DISTS>(L.lens, n, L.tab_wave, req, L.ts, root, used, lmin);
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        int rs = 0;
+        unsigned sroot = req, sused = 0, smin = 0;
+        if (lane == 0) rs = build_table(type, L.lens, n, L.tab_serial, &sroot, &sused, L.sorted, &smin);
+        rs = __shfl(rs, 0);
+        sroot = __shfl(sroot, 0);
+        sused = __shfl(sused, 0);
+        smin = __shfl(smin, 0);
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        for (unsigned i = lane; i < kEnough; i += 64) {
+            out_wave[(size_t)c * kEnough + i] = L.tab_wave[i];
+            out_serial[(size_t)c * kEnough + i] = L.tab_serial[i];
+        }
+        if (lane == 0) {
+            int32_t* mm = meta + c * 8;
+            mm[0] = r;
+            mm[1] = (int32_t)root;
+            mm[2] = (int32_t)used;
+            mm[3] = (int32_t)lmin;
+            mm[4] = rs;
+            mm[5] = (int32_t)sroot;
+            mm[6] = (int32_t)sused;
+            mm[7] = (int32_t)smin;
+        }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+    }
+}
+
+}  // namespace bpmd
+
+extern "C" int bpmd_diag_build_tables(const uint8_t* d_lens, const uint32_t* d_n, const int32_t* d_type,
+                                      uint32_t count, uint16_t* d_wave, uint16_t* d_serial, int32_t* d_meta,
+                                      void* stream)
+{
+    if (count == 0) return 0;
+    unsigned grid = count < 2048 ? count : 2048;
+    hipLaunchKernelGGL(bpmd::diag_tables_kernel, dim3(grid), dim3(64), 0, (hipStream_t)stream, d_lens, d_n, d_type,
+                       count, d_wave, d_serial, d_meta);
+    return (int)hipGetLastError();
+}

@@ -1,439 +1,696 @@
-// pmd_inflate.hip -- batched raw-DEFLATE decode for permessage-deflate
-// payloads on gfx950 (CDNA4).  One wavefront owns one message at a time.
+// pmd_inflate.hip -- batched raw-DEFLATE decode of permessage-deflate payloads
+// on gfx950 (CDNA4, wave64).  One wavefront owns one message at a time.
 //
-// Semantics follow Beast's decoder (include/boost/beast/zlib/detail/
-// inflate_stream.ipp:74-535) driven the way the websocket read path drives
-// it (websocket/detail/impl_base.hpp:168-190, websocket/impl/read.hpp:
-// 1284-1356): the payload plus an appended 00 00 FF FF tail is decoded from a
-// fresh state; decoding stops when the next step would need more bits than
-// the input holds (Beast's bitstream fill rule), on BFINAL (end_of_stream),
-// on the first data error (its zlib::error value), or when the output would
-// exceed the message's capacity (need_buffers, output truncated to the
-// capacity).
+// Reference semantics: Beast's decoder (include/boost/beast/zlib/detail/
+// inflate_stream.ipp:74-535) driven as the websocket read path drives it
+// (websocket/detail/impl_base.hpp:168-190, websocket/impl/read.hpp:1284-1356):
+// the payload plus an appended 00 00 FF FF tail is decoded from a fresh
+// state; decoding stops when the next step would need more bits than the
+// input holds (the bitstream fill rule, bitstream.hpp:109-121), on BFINAL
+// (end_of_stream), at the first data error (its zlib::error), or when the
+// output would exceed the slot capacity (need_buffers, output truncated).
 //
-// Memory: per wave, LDS holds the decode tables (16-bit slots, huff_table.h),
-// the code lengths and an output stage.  Messages whose output fits the stage
-// never touch global memory except for one coalesced store at the end;
-// larger ones flush the stage in STAGE-byte pieces and read older history
-// back from global memory.
+// Parallel decode.  Huffman decoding is serial within a stream, but a
+// Huffman-coded bit stream re-synchronises when decoding starts at a wrong
+// bit offset (on deflated JSON: 56 % of wrong starts within 8 tokens, 93 %
+// within 32).  Each round of a block cuts the remaining bits into 64
+// segments of ~32 tokens (estimated from the block's measured bits/token):
+//   pass A  every lane decodes its segment from the segment start
+//           (speculative for lanes >= 1) and records where it exits;
+//   pass B  lane l restarts at lane l-1's exit -- the true token boundary
+//           whenever lane l-1 re-synchronised -- and counts tokens/bytes;
+//           lanes whose start disagrees with the predecessor's exit are
+//           re-run until the chain is exact (lane 0 is exact by
+//           construction, and each re-run makes the first bad lane exact);
+//   pass C  after a prefix sum of the counts, lanes decode once more and
+//           store their tokens straight into stream order, checking each
+//           against its output position (invalid_distance, capacity).
+// The first lane with an event (end of block, error, end of input,
+// capacity) ends the round.  Tokens are then expanded 64 output bytes at a
+// time: each lane finds its token with one popcount over a token-start
+// bitmap, literal bytes are direct, match bytes read older output from the
+// LDS ring (or global memory beyond it), and matches reaching into the same
+// 64-byte chunk are resolved by pointer jumping across lanes (<= 6 steps).
+//
+// LDS per wave (~24 KiB): output ring, input window, round token list,
+// bitmap / header scratch (union), decode tables (huff_table.h slots).
 #include "pmd_common.h"
 #include "huff_table.h"
+#include "huff_wave.h"
 
 namespace bpmd {
 
-constexpr unsigned STAGE = 8192;          // output stage bytes per wave
-constexpr unsigned WAVES_PER_BLOCK = 4;
+constexpr unsigned RING = 8192;          // output history ring (bytes)
+constexpr unsigned RING_MASK = RING - 1;
+constexpr unsigned R_MAX = RING - 256;   // output bytes per round, at most
+constexpr unsigned IN_CAP = 2560;        // input window bytes
+constexpr unsigned IN_PAD = 32;
+constexpr unsigned WIN_WORDS = (IN_CAP + IN_PAD) / 4;
+constexpr unsigned TOT = 2048;           // tokens per round, at most
+constexpr unsigned SEG_TOKENS = 32;      // target tokens per lane segment
+constexpr unsigned SEG_MAX_BITS = 300;   // keeps a round inside the window
+constexpr unsigned BM_WORDS = (R_MAX + 128) / 32 + 2;
+
+enum Ev : uint32_t { EV_NONE = 0, EV_EOB, EV_ERROR, EV_STARVED, EV_FULL, EV_PARTIAL };
 
 struct alignas(16) WaveLds {
-    uint8_t stage[STAGE];                   // 16-byte aligned (first member)
-    uint16_t tab[kEnough];                  // lens table then dists table
-    uint16_t sorted[320];
-    uint8_t lens[320];
+    uint8_t ring[RING];
+    uint32_t win[WIN_WORDS];
+    uint32_t tok[TOT];
+    union {
+        uint32_t bitmap[BM_WORDS];
+        struct {
+            WaveTableScratch ts;
+            uint8_t lens[320];
+        } h;
+    } u;
+    uint16_t tab[kEnough];
 };
 
-// fixed-Huffman tables built once on the host with the same builder
 __device__ uint16_t g_fixed_lens[512];
 __device__ uint16_t g_fixed_dists[32];
 
-struct InMsg {
+// Diagnostic build only (-DBPMD_PROF): per-phase cycle and event counters.
+__device__ unsigned long long g_prof[16];
+#ifdef BPMD_PROF
+#define PROF_DECL unsigned long long prof_[16] = {0}; unsigned long long prof_t_ = __builtin_amdgcn_s_memtime()
+#define PROF_MARK() (prof_t_ = __builtin_amdgcn_s_memtime())
+#define PROF_LAP(i) do { unsigned long long t2_ = __builtin_amdgcn_s_memtime(); prof_[i] += t2_ - prof_t_; prof_t_ = t2_; } while (0)
+#define PROF_CNT(i, n) (prof_[i] += (n))
+#define PROF_FLUSH() do { if (lane_id() == 0) for (int i_ = 0; i_ < 16; ++i_) atomicAdd(&g_prof[i_], prof_[i_]); } while (0)
+#else
+#define PROF_DECL
+#define PROF_MARK()
+#define PROF_LAP(i)
+#define PROF_CNT(i, n)
+#define PROF_FLUSH()
+#endif
+
+struct Msg {
     const uint8_t* p;
-    uint32_t n;        // payload bytes
-    uint32_t total;    // payload + tail bytes (4 unless raw)
+    uint32_t n;       // payload bytes
+    uint32_t total;   // payload + tail bytes
 };
 
-__device__ __forceinline__ uint32_t in_byte(const InMsg& m, uint32_t i)
+__device__ __forceinline__ uint32_t in_byte(const Msg& m, uint32_t i)
 {
     if (i < m.n) return m.p[i];
     if (i < m.total) return (i - m.n) >= 2 ? 0xffu : 0u;   // 00 00 FF FF
     return 0;
 }
 
-// 4 bytes of the virtual stream (payload || tail || zeros) at byte offset i
-__device__ __forceinline__ uint32_t in_word(const InMsg& m, uint32_t i)
+// 4 bytes of payload || tail || zeros at byte offset i
+__device__ __forceinline__ uint32_t in_word(const Msg& m, uint32_t i)
 {
     if (i + 8 <= m.n) {
         uintptr_t a = (uintptr_t)(m.p + i);
         const uint32_t* w = (const uint32_t*)(a & ~(uintptr_t)3);
-        unsigned sh = (unsigned)(a & 3) * 8;
-        uint64_t v = ((uint64_t)w[1] << 32) | w[0];
+        const unsigned sh = (unsigned)(a & 3) * 8;
+        const uint64_t v = ((uint64_t)w[1] << 32) | w[0];
         return (uint32_t)(v >> sh);
     }
     return in_byte(m, i) | (in_byte(m, i + 1) << 8) | (in_byte(m, i + 2) << 16) | (in_byte(m, i + 3) << 24);
 }
 
-// LSB-first bit reader over the virtual stream (wave-uniform state)
-struct Bits {
-    uint64_t buf;
-    uint32_t cnt;      // valid bits in buf
-    uint32_t next;     // next byte offset to load
-    uint32_t total_bits;
-    __device__ __forceinline__ void refill(const InMsg& m)
-    {
-        if (cnt <= 32) {
-            buf |= (uint64_t)in_word(m, next) << cnt;
-            next += 4;
-            cnt += 32;
-        }
-    }
-    __device__ __forceinline__ uint32_t pos() const { return next * 8 - cnt; }
-    __device__ __forceinline__ uint32_t avail() const
-    {
-        uint32_t p = pos();
-        return p < total_bits ? total_bits - p : 0;
-    }
-    __device__ __forceinline__ uint32_t peek(unsigned n) const { return (uint32_t)(buf & ((1ull << n) - 1)); }
-    __device__ __forceinline__ void drop(unsigned n) { buf >>= n; cnt -= n; }
-    __device__ __forceinline__ uint32_t take(unsigned n)
-    {
-        uint32_t v = peek(n);
-        drop(n);
-        return v;
-    }
+// 64 stream bits starting at bit p_rel of the LDS window
+__device__ __forceinline__ uint64_t peek64(const uint32_t* win, uint32_t p_rel)
+{
+    const uint32_t w = p_rel >> 5, sh = p_rel & 31;
+    const uint32_t d0 = win[w], d1 = win[w + 1], d2 = win[w + 2];
+    const uint32_t lo = __builtin_amdgcn_alignbit(d1, d0, sh);
+    const uint32_t hi = __builtin_amdgcn_alignbit(d2, d1, sh);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint32_t lowbits(uint64_t v, unsigned n) { return (uint32_t)v & ((1u << n) - 1u); }
+
+// byte of our own earlier output, read past the (non-coherent) L1
+__device__ __forceinline__ uint32_t gbyte(const uint8_t* p)
+{
+    const uintptr_t a = (uintptr_t)p;
+    uint32_t* w = (uint32_t*)(a & ~(uintptr_t)3);
+    const uint32_t v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return (v >> ((a & 3) * 8)) & 0xffu;
+}
+
+__device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); asm volatile("" ::: "memory"); }
+
+// ------------------------------------------------------------- token decode
+
+struct Tok {
+    uint32_t info;    // literal: byte;  match: (len << 16) | dist
+    uint32_t nbits;
+    uint32_t olen;    // output bytes
+    uint32_t ev;      // EV_NONE, EV_EOB, EV_ERROR, EV_STARVED
+    uint32_t err;
 };
 
-// Output: stage in LDS, history beyond the stage in global memory.
-struct Out {
-    uint8_t* g;          // message output slot
-    uint32_t cap;
-    uint32_t pos;        // bytes produced
-    uint32_t base;       // absolute position of stage[0]
-    uint8_t* stage;
-};
-
-__device__ void flush_stage(Out& o, uint32_t upto)
+// One literal/length[/distance] token from the 64 stream bits v with Beast's
+// fill rule: each step needs the bits the reference's slow path asks for
+// (inflate_stream.ipp:360-474).  avail = bits left in the stream.
+__device__ __forceinline__ Tok decode_tok(uint64_t v, uint32_t avail, const uint16_t* ltab, unsigned lroot,
+                                          const uint16_t* dtab, unsigned droot)
 {
-    // copy stage[0, upto-base) to global [base, upto)
-    const unsigned lane = lane_id();
-    uint32_t n = upto - o.base;
-    uint8_t* dst = o.g + o.base;
-    if ((((uintptr_t)dst) & 15) == 0) {
-        uint32_t n16 = n & ~15u;
-        for (uint32_t i = lane * 16; i < n16; i += WAVE * 16)
-            *(uint4*)(dst + i) = *(const uint4*)(o.stage + i);
-        for (uint32_t i = n16 + lane; i < n; i += WAVE) dst[i] = o.stage[i];
-    } else {
-        for (uint32_t i = lane; i < n; i += WAVE) dst[i] = o.stage[i];
-    }
-    __builtin_amdgcn_s_waitcnt(0);   // stores visible to this wave's later loads
-    __threadfence_block();
-}
-
-__device__ __forceinline__ uint8_t out_read(const Out& o, uint32_t q)
-{
-    return q >= o.base ? o.stage[q - o.base] : o.g[q];
-}
-
-// make room so that [pos, pos+n) fits in the stage (n <= STAGE/2)
-__device__ __forceinline__ void stage_room(Out& o, uint32_t n)
-{
-    if (o.pos + n - o.base > STAGE) {
-        // keep the stage aligned to STAGE/2 so the tail stays resident
-        uint32_t keep_from = o.pos & ~(STAGE / 2 - 1);
-        if (keep_from > o.base) {
-            flush_stage(o, keep_from);
-            uint32_t shift = keep_from - o.base;
-            uint32_t live = o.pos - keep_from;
-            const unsigned lane = lane_id();
-            for (uint32_t i = lane; i < live; i += WAVE) {
-                uint8_t c = o.stage[shift + i];
-                __builtin_amdgcn_wave_barrier();
-                o.stage[i] = c;
-            }
-            __builtin_amdgcn_wave_barrier();
-            o.base = keep_from;
-        }
-    }
-}
-
-// wave-parallel match copy: out[pos + k] = out[pos - dist + (k mod dist)]
-__device__ __forceinline__ void copy_match(Out& o, uint32_t len, uint32_t dist)
-{
-    const unsigned lane = lane_id();
-    uint32_t start = o.pos;
-    if (dist >= len) {
-        for (uint32_t k = lane; k < len; k += WAVE) {
-            uint8_t c = out_read(o, start - dist + k);
-            o.stage[start + k - o.base] = c;
-        }
-    } else {
-        // overlapping: rounds of min(dist, 64) bytes, each round reads only
-        // bytes finished by earlier rounds
-        uint32_t step = dist < WAVE ? dist : WAVE;
-        for (uint32_t k0 = 0; k0 < len; k0 += step) {
-            uint32_t k = k0 + lane;
-            uint8_t c = 0;
-            if (lane < step && k < len) c = out_read(o, start - dist + k);
-            __builtin_amdgcn_wave_barrier();
-            if (lane < step && k < len) o.stage[start + k - o.base] = c;
-            __builtin_amdgcn_wave_barrier();
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-    o.pos = start + len;
-}
-
-// Decode one symbol with Beast's fill rule.  Returns false when the input
-// cannot supply the bits the reference would ask for.
-__device__ __forceinline__ bool decode_sym(Bits& b, const InMsg& m, const uint16_t* tab, unsigned root,
-                                           uint16_t& out)
-{
-    b.refill(m);
-    uint32_t av = b.avail();
-    if (av < root) return false;
-    uint16_t s = tab[b.peek(root)];
+    Tok t;
+    t.info = 0;
+    t.nbits = 0;
+    t.olen = 0;
+    t.ev = EV_NONE;
+    t.err = 0;
+    uint16_t s = ltab[lowbits(v, lroot)];
+    unsigned need = lroot, used;
     if (slot_is_link(s)) {
-        unsigned sub = slot_bits(s);
-        if (av < root + sub) return false;
-        uint16_t t = tab[slot_val(s) + ((b.peek(root + sub)) >> root)];
-        b.drop(root + slot_bits(t));
-        out = t;
-        return true;
+        const unsigned sub = slot_bits(s);
+        need = lroot + sub;
+        s = ltab[slot_val(s) + lowbits(v >> lroot, sub)];
+        used = lroot + slot_bits(s);
+    } else {
+        used = slot_bits(s);
     }
-    b.drop(slot_bits(s));
-    out = s;
-    return true;
+    if (avail < need) { t.ev = EV_STARVED; return t; }
+    const unsigned kind = slot_kind(s);
+    if (kind == K_VAL) {
+        t.info = slot_val(s);
+        t.nbits = used;
+        t.olen = 1;
+        return t;
+    }
+    if (kind == K_EOB) { t.ev = EV_EOB; t.nbits = used; return t; }
+    if (kind == K_SPECIAL) { t.ev = EV_ERROR; t.err = ST_INVALID_LITERAL_LENGTH; return t; }
+    // length (RFC 1951 3.2.5): base and extra bits from the symbol index
+    const unsigned li = slot_val(s);
+    const unsigned xl = (li < 8 || li == 28) ? 0u : ((li - 4) >> 2);
+    unsigned len = li < 8 ? li + 3 : (li == 28 ? 258u : (((4u + (li & 3)) << xl) + 3));
+    len += lowbits(v >> used, xl);
+    used += xl;
+    if (avail < used) { t.ev = EV_STARVED; return t; }
+    uint16_t d = dtab[lowbits(v >> used, droot)];
+    need = used + droot;
+    unsigned dused;
+    if (slot_is_link(d)) {
+        const unsigned sub = slot_bits(d);
+        need += sub;
+        d = dtab[slot_val(d) + lowbits(v >> (used + droot), sub)];
+        dused = used + droot + slot_bits(d);
+    } else {
+        dused = used + slot_bits(d);
+    }
+    if (avail < need) { t.ev = EV_STARVED; return t; }
+    if (slot_kind(d) == K_SPECIAL) { t.ev = EV_ERROR; t.err = ST_INVALID_DISTANCE_CODE; return t; }
+    const unsigned di = slot_val(d);
+    const unsigned xd = di < 4 ? 0u : (di >> 1) - 1;
+    unsigned dist = di < 4 ? di + 1 : (((2u + (di & 1)) << xd) + 1);
+    dist += lowbits(v >> dused, xd);
+    dused += xd;
+    if (avail < dused) { t.ev = EV_STARVED; return t; }
+    t.info = (len << 16) | dist;
+    t.nbits = dused;
+    t.olen = len;
+    return t;
 }
 
-static const __constant__ uint8_t kClenOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+struct LaneRes {
+    uint32_t exit, n, bytes, ev, err;
+};
 
-// One message; all lanes run the same control flow (uniform state).
-// raw: plain zlib::inflate_stream::write() semantics (no tail; a full output
-// buffer ends the call without error).  Otherwise the pmd message semantics:
-// producing byte cap+1 reports need_buffers.
-__device__ void inflate_one(WaveLds& L, const InMsg& m, Out& o, uint32_t& out_len, int32_t& status, bool raw)
+struct Tables {
+    const uint16_t* ltab;
+    const uint16_t* dtab;
+    unsigned lroot, droot;
+};
+
+// Count pass: decode tokens starting at `start` until a token would start
+// at or beyond `end`, or an event.
+__device__ __forceinline__ LaneRes decode_count(const WaveLds& L, uint32_t wb, uint32_t start, uint32_t end,
+                                                uint32_t total_bits, const Tables& T)
 {
-    const int32_t full_status = raw ? ST_OK : ST_NEED_BUFFERS;
-    const unsigned lane = lane_id();
-    Bits b;
-    b.buf = 0;
-    b.cnt = 0;
-    b.next = 0;
-    b.total_bits = m.total * 8;
-    int st = ST_OK;
-    bool last = false;
+    LaneRes r;
+    r.n = 0;
+    r.bytes = 0;
+    r.ev = EV_NONE;
+    r.err = 0;
+    uint32_t p = start;
+    while (p < end) {
+        const uint64_t v = peek64(L.win, p - wb);
+        const uint32_t avail = p < total_bits ? total_bits - p : 0;
+        const Tok t = decode_tok(v, avail, T.ltab, T.lroot, T.dtab, T.droot);
+        if (t.ev != EV_NONE) {
+            r.ev = t.ev;
+            r.err = t.err;
+            if (t.ev == EV_EOB) p += t.nbits;
+            break;
+        }
+        r.n += 1;
+        r.bytes += t.olen;
+        p += t.nbits;
+    }
+    r.exit = p;
+    return r;
+}
 
-    if (m.total == 0) {            // raw mode, empty input: no progress
+// Store pass: the same decode from an exact start, writing tokens at
+// tok[P...] and their output offsets into the bitmap, with the checks the
+// reference makes at each token's output position (inflate_stream.ipp:
+// 475-514): a full buffer first when the capacity is exact (raw), then the
+// distance, then the capacity.
+__device__ __forceinline__ LaneRes decode_store(WaveLds& L, uint32_t wb, uint32_t start, uint32_t end,
+                                                uint32_t total_bits, const Tables& T, uint32_t P, uint32_t abs0,
+                                                uint32_t round0, uint32_t cap, bool raw)
+{
+    LaneRes r;
+    r.n = 0;
+    r.bytes = 0;
+    r.ev = EV_NONE;
+    r.err = 0;
+    uint32_t p = start;
+    while (p < end) {
+        const uint64_t v = peek64(L.win, p - wb);
+        const uint32_t avail = p < total_bits ? total_bits - p : 0;
+        const Tok t = decode_tok(v, avail, T.ltab, T.lroot, T.dtab, T.droot);
+        if (t.ev != EV_NONE) {
+            r.ev = t.ev;
+            r.err = t.err;
+            if (t.ev == EV_EOB) p += t.nbits;
+            break;
+        }
+        const uint32_t abs = abs0 + r.bytes;
+        if (raw && abs >= cap) { r.ev = EV_FULL; break; }
+        if (t.olen > 1 || (t.info >> 16)) {
+            if ((t.info & 0xffffu) > abs) { r.ev = EV_ERROR; r.err = ST_INVALID_DISTANCE; break; }
+        }
+        if (abs >= cap) { r.ev = EV_FULL; break; }
+        L.tok[P + r.n] = t.info;
+        const uint32_t rel = abs - round0;
+        atomicOr(&L.u.bitmap[rel >> 5], 1u << (rel & 31));
+        r.n += 1;
+        p += t.nbits;
+        if (abs + t.olen > cap) {
+            r.bytes += cap - abs;
+            r.ev = EV_PARTIAL;
+            break;
+        }
+        r.bytes += t.olen;
+    }
+    r.exit = p;
+    return r;
+}
+
+// --------------------------------------------------------------- wave utils
+
+__device__ __forceinline__ uint32_t scan_incl(uint32_t x)
+{
+    const unsigned lane = lane_id();
+#pragma unroll
+    for (unsigned d = 1; d < WAVE; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+    }
+    return x;
+}
+
+__device__ __forceinline__ uint32_t from_prev_lane(uint32_t x) { return __shfl_up(x, 1); }
+
+__device__ __forceinline__ unsigned first_lane(uint64_t mask) { return mask ? (unsigned)__builtin_ctzll(mask) : WAVE; }
+
+// ------------------------------------------------------------------- output
+
+struct Out {
+    uint8_t* g;       // message slot in global memory
+    uint32_t cap;
+    uint32_t pos;     // bytes produced
+    uint32_t flushed; // bytes already stored to g
+};
+
+// store ring bytes [a, b) to global memory
+__device__ void ring_flush(WaveLds& L, Out& o, uint32_t a, uint32_t b)
+{
+    if (b <= a) return;
+    const unsigned lane = lane_id();
+    if ((((uintptr_t)o.g) & 15) == 0) {
+        const uint32_t a16 = (a + 15) & ~15u, b16 = b & ~15u;
+        if (a16 < b16) {
+            for (uint32_t i = a + lane; i < a16; i += WAVE) o.g[i] = L.ring[i & RING_MASK];
+            for (uint32_t q = a16 + lane * 16; q < b16; q += WAVE * 16)
+                *(uint4*)(o.g + q) = *(const uint4*)(L.ring + (q & RING_MASK));
+            for (uint32_t i = b16 + lane; i < b; i += WAVE) o.g[i] = L.ring[i & RING_MASK];
+            return;
+        }
+    }
+    for (uint32_t i = a + lane; i < b; i += WAVE) o.g[i] = L.ring[i & RING_MASK];
+}
+
+// positions about to be overwritten in the ring must reach global memory
+__device__ __forceinline__ void ring_reserve(WaveLds& L, Out& o, uint32_t n)
+{
+    const uint32_t need = o.pos + n;
+    if (need > RING && need - RING > o.flushed) {
+        ring_flush(L, o, o.flushed, need - RING);
+        o.flushed = need - RING;
+        __builtin_amdgcn_s_waitcnt(0);
+        wave_sync();
+    }
+}
+
+// expand the round's tokens into output bytes [o.pos, o.pos + nbytes)
+__device__ __forceinline__ void expand_round(WaveLds& L, Out& o, uint32_t nbytes)
+{
+    const unsigned lane = lane_id();
+    ring_reserve(L, o, nbytes);
+    const uint32_t rs = o.pos, re = o.pos + nbytes;
+    int32_t tprev = -1;
+    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+    for (uint32_t c = rs; c < re; c += WAVE) {
+        const uint32_t rel = c - rs;   // multiple of 64
+        const uint64_t B = ((uint64_t)L.u.bitmap[(rel >> 5) + 1] << 32) | L.u.bitmap[rel >> 5];
+        const uint32_t q = c + lane;
+        const bool act = q < re;
+        // ring slots written by this chunk hold positions < wend - RING
+        const uint32_t wend = c + WAVE < re ? c + WAVE : re;
+        const int32_t T = tprev + (int32_t)__builtin_popcountll(B & upto);
+        const uint32_t info = act ? L.tok[T] : 0u;
+        const uint32_t len = info >> 16;
+        uint32_t val = info & 0xffu;
+        uint32_t src = q - (info & 0xffffu);
+        bool pend = false;
+        if (act && len) {
+            if (src >= c) pend = true;
+            else if (src + RING >= wend) val = L.ring[src & RING_MASK];
+            else val = gbyte(o.g + src);
+        }
+        // matches reaching into this chunk: pointer jumping
+        while (__ballot(pend)) {
+            const unsigned from = pend ? src - c : lane;
+            const uint32_t v2 = __shfl(val, from);
+            const uint32_t s2 = __shfl(src, from);
+            const bool p2 = __shfl(pend ? 1 : 0, from) != 0;
+            if (pend) {
+                if (!p2) { val = v2; pend = false; }
+                else src = s2;
+            }
+        }
+        if (act) L.ring[q & RING_MASK] = (uint8_t)val;
+        tprev += (int32_t)__builtin_popcountll(B);
+        wave_sync();
+    }
+    o.pos = re;
+}
+
+// --------------------------------------------------------------- one message
+
+static __constant__ const uint8_t kClenOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+__device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t& out_len, int32_t& status)
+{
+    const unsigned lane = lane_id();
+    const uint32_t total_bits = m.total * 8;
+    int32_t st = ST_OK;
+    const int32_t full_status = raw ? ST_OK : ST_NEED_BUFFERS;
+    if (m.total == 0) {   // raw mode, no input: no progress (inflate_stream.ipp:113-117)
         out_len = 0;
         status = ST_NEED_BUFFERS;
         return;
     }
+    PROF_DECL;
+    uint32_t wbase = 0;   // window start, bytes (multiple of 4)
+    for (uint32_t i = lane; i < WIN_WORDS; i += WAVE) L.win[i] = in_word(m, 4 * i);
+    wave_sync();
+    PROF_LAP(10);
+    auto ensure = [&](uint32_t p, uint32_t nbytes) {
+        const uint32_t b0 = p >> 3;
+        if (b0 < wbase || b0 + nbytes > wbase + IN_CAP) {
+            PROF_MARK();
+            wbase = b0 & ~3u;
+            wave_sync();
+            for (uint32_t i = lane; i < WIN_WORDS; i += WAVE) L.win[i] = in_word(m, wbase + 4 * i);
+            wave_sync();
+            PROF_LAP(10);
+            PROF_CNT(11, 1);
+        }
+    };
+    auto ubits = [&](uint32_t p, unsigned n) -> uint32_t { return lowbits(peek64(L.win, p - wbase * 8), n); };
+
+    uint32_t pos = 0;    // stream bit position (wave-uniform)
+    bool last = false;
+    uint32_t est16 = 8 * 16;   // estimated bits per token, x16
 
     for (;;) {
         // ---- TYPEDO (inflate_stream.ipp:146-182)
         if (last) { st = ST_END_OF_STREAM; break; }
-        b.refill(m);
-        if (b.avail() < 3) break;
-        last = b.take(1) != 0;
-        unsigned type = b.take(2);
-        unsigned lroot = 9, droot = 6;
-        const uint16_t* ltab = L.tab;
-        const uint16_t* dtab = L.tab;
+        ensure(pos, 700);
+        if (total_bits - pos < 3) break;
+        const uint32_t hdr = ubits(pos, 3);
+        pos += 3;
+        last = (hdr & 1) != 0;
+        const unsigned type = hdr >> 1;
+        Tables T;
+        T.ltab = L.tab;
+        T.dtab = L.tab + 512;
+        T.lroot = 9;
+        T.droot = 5;
+
         if (type == 0) {
             // ---- STORED / COPY (ipp:184-220)
-            b.drop(b.cnt & 7);
-            if (b.avail() < 32) break;
-            b.refill(m);
-            uint32_t v = b.take(16);
-            uint32_t nv = b.take(16);
+            pos = (pos + 7) & ~7u;
+            if (pos > total_bits || total_bits - pos < 32) break;
+            const uint32_t v = ubits(pos, 16), nv = ubits(pos + 16, 16);
             if (v != (nv ^ 0xffffu)) { st = ST_INVALID_STORED_LENGTH; break; }
-            // bytes left in the reservoir are whole bytes; rewind them
-            uint32_t from = b.next - b.cnt / 8;
-            b.buf = 0;
-            b.cnt = 0;
-            uint32_t have = m.total > from ? m.total - from : 0;
+            pos += 32;
+            const uint32_t from = pos >> 3;
+            const uint32_t have = m.total - from;
             uint32_t n = v < have ? v : have;
-            bool overflow = false;
-            if (o.pos + n > o.cap) { n = o.cap - o.pos; overflow = true; }
-            // copy in pieces that fit the stage
-            uint32_t done = 0;
-            while (done < n) {
-                uint32_t piece = n - done;
-                if (piece > STAGE / 2) piece = STAGE / 2;
-                stage_room(o, piece);
+            bool full = false;
+            if (o.pos + n > o.cap) { n = o.cap - o.pos; full = true; }
+            for (uint32_t done = 0; done < n;) {
+                const uint32_t piece = n - done < R_MAX ? n - done : R_MAX;
+                ring_reserve(L, o, piece);
                 for (uint32_t k = lane; k < piece; k += WAVE)
-                    o.stage[o.pos + k - o.base] = (uint8_t)in_byte(m, from + done + k);
-                __builtin_amdgcn_wave_barrier();
+                    L.ring[(o.pos + k) & RING_MASK] = (uint8_t)in_byte(m, from + done + k);
+                wave_sync();
                 o.pos += piece;
                 done += piece;
             }
-            b.next = from + n;
-            if (overflow) { st = full_status; break; }
-            if (n < v) break;            // input ran out inside the block
+            pos += n * 8;
+            if (full) { st = full_status; break; }
+            if (n < v) break;   // input ends inside the block
             continue;
         } else if (type == 1) {
-            // fixed tables: copy into the wave's table space
             for (unsigned k = lane; k < 512; k += WAVE) L.tab[k] = g_fixed_lens[k];
-            for (unsigned k = lane; k < 32; k += WAVE) L.tab[512 + k] = g_fixed_dists[k];
-            __builtin_amdgcn_wave_barrier();
-            lroot = 9;
-            droot = 5;
-            dtab = L.tab + 512;
+            if (lane < 32) L.tab[512 + lane] = g_fixed_dists[lane];
+            wave_sync();
         } else if (type == 2) {
             // ---- TABLE / LENLENS / CODELENS (ipp:222-354)
-            b.refill(m);
-            if (b.avail() < 14) break;
-            unsigned nlen = b.take(5) + 257;
-            unsigned ndist = b.take(5) + 1;
-            unsigned ncode = b.take(4) + 4;
+            if (total_bits - pos < 14) break;
+            const unsigned nlen = ubits(pos, 5) + 257;
+            const unsigned ndist = ubits(pos + 5, 5) + 1;
+            const unsigned ncode = ubits(pos + 10, 4) + 4;
+            pos += 14;
             if (nlen > 286 || ndist > 30) { st = ST_TOO_MANY_SYMBOLS; break; }
-            bool starved = false;
-            if (lane < 19) L.lens[lane] = 0;
-            __builtin_amdgcn_wave_barrier();
-            for (unsigned i = 0; i < ncode; ++i) {
-                b.refill(m);
-                if (b.avail() < 3) { starved = true; break; }
-                unsigned v = b.take(3);
-                if (lane == 0) L.lens[kClenOrder[i]] = (uint8_t)v;
+            // the code-length code lengths: lane i reads field i
+            if (total_bits - pos < 3 * ncode) {
+                // the reference reads them one by one and stops when starved
+                break;
             }
-            if (starved) break;
-            __builtin_amdgcn_wave_barrier();
-            unsigned croot = 7, used = 0;
-            int r = 0;
-            if (lane == 0) r = build_table(BUILD_CODES, L.lens, 19, L.tab, &croot, &used, L.sorted);
-            r = __shfl(r, 0);
-            croot = __shfl(croot, 0);
-            __builtin_amdgcn_wave_barrier();
+            if (lane < 19) {
+                uint32_t cl = 0;
+                for (unsigned i = 0; i < ncode; ++i)
+                    if (kClenOrder[i] == lane) cl = ubits(pos + 3 * i, 3);
+                L.u.h.lens[lane] = (uint8_t)cl;
+            }
+            pos += 3 * ncode;
+            wave_sync();
+            unsigned croot = 0, cused = 0, cmin = 0;
+            int r = build_table_wave<BUILD_CODES>(L.u.h.lens, 19, L.tab, 7, L.u.h.ts, croot, cused, cmin);
+            wave_sync();
             if (r) { st = r; break; }
+            bool starved = false;
             unsigned have = 0;
             while (have < nlen + ndist) {
-                uint16_t s;
-                if (!decode_sym(b, m, L.tab, croot, s)) { starved = true; break; }
-                unsigned sym = slot_val(s);
+                if (total_bits - pos < croot) { starved = true; break; }
+                const uint16_t s = L.tab[ubits(pos, croot)];
+                const unsigned sym = slot_val(s);
+                const unsigned cb = slot_bits(s);
                 if (sym < 16) {
-                    if (lane == 0) L.lens[have] = (uint8_t)sym;
+                    pos += cb;
+                    if (lane == 0) L.u.h.lens[have] = (uint8_t)sym;
                     ++have;
                     continue;
                 }
-                // repeat codes: the reference asks for code+extra bits at once
-                // (ipp:282-312); the code bits were already consumed above, so
-                // ask for the extra bits only
-                unsigned xb = sym == 16 ? 2 : sym == 17 ? 3 : 7;
-                b.refill(m);
-                if (b.avail() < xb) { starved = true; break; }
-                unsigned rep, val;
+                // the reference asks for code + extra bits together (ipp:282-312)
+                const unsigned xb = sym == 16 ? 2 : sym == 17 ? 3 : 7;
+                if (total_bits - pos < cb + xb) { starved = true; break; }
+                const uint32_t x = ubits(pos + cb, xb);
+                pos += cb + xb;
+                unsigned rep, val = 0;
                 if (sym == 16) {
                     if (have == 0) { st = ST_INVALID_BIT_LENGTH_REPEAT; break; }
-                    rep = 3 + b.take(2);
-                    __builtin_amdgcn_wave_barrier();
-                    val = L.lens[have - 1];
-                } else if (sym == 17) {
-                    rep = 3 + b.take(3);
-                    val = 0;
+                    rep = 3 + x;
+                    wave_sync();
+                    val = L.u.h.lens[have - 1];
                 } else {
-                    rep = 11 + b.take(7);
-                    val = 0;
+                    rep = (sym == 17 ? 3 : 11) + x;
                 }
                 if (have + rep > nlen + ndist) { st = ST_INVALID_BIT_LENGTH_REPEAT; break; }
-                for (unsigned k = lane; k < rep; k += WAVE) L.lens[have + k] = (uint8_t)val;
-                __builtin_amdgcn_wave_barrier();
+                for (unsigned k = lane; k < rep; k += WAVE) L.u.h.lens[have + k] = (uint8_t)val;
                 have += rep;
+                wave_sync();
             }
             if (st) break;
             if (starved) break;
-            __builtin_amdgcn_wave_barrier();
-            if (L.lens[256] == 0) { st = ST_MISSING_EOB; break; }
-            lroot = 9;
-            droot = 6;
-            unsigned lused = 0, dused = 0;
-            int r1 = 0, r2 = 0;
-            if (lane == 0) {
-                r1 = build_table(BUILD_LENS, L.lens, nlen, L.tab, &lroot, &lused, L.sorted);
-                if (!r1) r2 = build_table(BUILD_DISTS, L.lens + nlen, ndist, L.tab + lused, &droot, &dused, L.sorted);
-            }
-            r1 = __shfl(r1, 0);
-            r2 = __shfl(r2, 0);
-            lroot = __shfl(lroot, 0);
-            droot = __shfl(droot, 0);
-            lused = __shfl(lused, 0);
-            __builtin_amdgcn_wave_barrier();
-            if (r1) { st = r1; break; }
-            if (r2) { st = r2; break; }
-            dtab = L.tab + lused;
+            wave_sync();
+            if (L.u.h.lens[256] == 0) { st = ST_MISSING_EOB; break; }
+            unsigned lroot = 0, lused = 0, lmin = 0, droot = 0, dused = 0, dmin = 0;
+            r = build_table_wave<BUILD_LENS>(L.u.h.lens, nlen, L.tab, 9, L.u.h.ts, lroot, lused, lmin);
+            wave_sync();
+            if (r) { st = r; break; }
+            r = build_table_wave<BUILD_DISTS>(L.u.h.lens + nlen, ndist, L.tab + lused, 6, L.u.h.ts, droot, dused,
+                                              dmin);
+            wave_sync();
+            if (r) { st = r; break; }
+            T.lroot = lroot;
+            T.droot = droot;
+            T.dtab = L.tab + lused;
         } else {
             st = ST_INVALID_BLOCK_TYPE;
             break;
         }
 
-        // ---- LEN ... MATCH (ipp:356-514)
-        bool block_end = false;
-        for (;;) {
-            uint16_t s;
-            if (!decode_sym(b, m, ltab, lroot, s)) break;
-            unsigned kind = slot_kind(s);
-            if (kind == K_VAL) {
-                if (o.pos >= o.cap) { st = full_status; break; }
-                stage_room(o, 1);
-                if (lane == 0) o.stage[o.pos - o.base] = (uint8_t)slot_val(s);
-                __builtin_amdgcn_wave_barrier();
-                o.pos += 1;
-                continue;
+        // ---- compressed data, in rounds (ipp:356-514)
+        PROF_LAP(1);
+        PROF_CNT(8, 1);
+        bool stop = false, block_end = false;
+        uint32_t shrink = 0;
+        while (!stop && !block_end) {
+            PROF_CNT(6, 1);
+            const uint32_t S = pos;
+            const uint32_t rem = total_bits > S ? total_bits - S : 0;
+            uint32_t Lseg = (SEG_TOKENS * est16) >> 4;
+            if (Lseg > SEG_MAX_BITS) Lseg = SEG_MAX_BITS;
+            Lseg >>= shrink;
+            if ((uint64_t)Lseg * WAVE > rem) Lseg = (rem + WAVE - 1) / WAVE;
+            if (Lseg == 0) Lseg = 1;
+            ensure(S, (WAVE * Lseg + 160) / 8 + 16);
+            const uint32_t wb = wbase * 8;
+            const uint32_t seg0 = S + lane * Lseg, seg1 = seg0 + Lseg;
+
+            PROF_MARK();
+            const LaneRes a = decode_count(L, wb, seg0, seg1, total_bits, T);
+            PROF_LAP(2);
+            uint32_t start = lane == 0 ? S : from_prev_lane(a.exit);
+            LaneRes b = decode_count(L, wb, start, seg1, total_bits, T);
+            unsigned k;   // last lane of the round
+            for (;;) {
+                PROF_CNT(7, 1);
+                const uint32_t prev_exit = from_prev_lane(b.exit);
+                const bool bad = lane > 0 && start != prev_exit;
+                const uint64_t evm = __ballot(b.ev != EV_NONE);
+                const uint64_t badm = __ballot(bad);
+                const unsigned fe = first_lane(evm), fb = first_lane(badm);
+                if (fb > fe || fb == WAVE) {
+                    k = fe == WAVE ? WAVE - 1 : fe;
+                    break;
+                }
+                if (bad) {
+                    start = prev_exit;
+                    b = decode_count(L, wb, start, seg1, total_bits, T);
+                }
             }
-            if (kind == K_EOB) { block_end = true; break; }
-            if (kind == K_SPECIAL) { st = ST_INVALID_LITERAL_LENGTH; break; }
-            unsigned li = slot_val(s);
-            unsigned len = kLenBase[li];
-            unsigned xb = kLenExtra[li];
-            if (xb) {
-                b.refill(m);
-                if (b.avail() < xb) break;
-                len += b.take(xb);
+            PROF_LAP(3);
+            // token and byte offsets within the round; keep the round within
+            // the token list and the ring
+            uint32_t nn = lane <= k ? b.n : 0, bb = lane <= k ? b.bytes : 0;
+            uint32_t n_incl = scan_incl(nn), b_incl = scan_incl(bb);
+            {
+                const uint64_t over = __ballot(lane <= k && (n_incl > TOT || b_incl > R_MAX));
+                const unsigned fo = first_lane(over);
+                if (fo == 0) {          // one lane alone is too big: shorter segments
+                    ++shrink;
+                    continue;
+                }
+                if (fo <= k) k = fo - 1;
             }
-            if (!decode_sym(b, m, dtab, droot, s)) break;
-            if (slot_kind(s) == K_SPECIAL) { st = ST_INVALID_DISTANCE_CODE; break; }
-            unsigned di = slot_val(s);
-            unsigned dist = kDistBase[di];
-            xb = kDistExtra[di];
-            if (xb) {
-                b.refill(m);
-                if (b.avail() < xb) break;
-                dist += b.take(xb);
+            const uint32_t P = n_incl - nn, O = b_incl - bb;
+            for (unsigned i = lane; i < BM_WORDS; i += WAVE) L.u.bitmap[i] = 0;
+            wave_sync();
+            LaneRes c;
+            c.exit = start;
+            c.n = 0;
+            c.bytes = 0;
+            c.ev = EV_NONE;
+            c.err = 0;
+            if (lane <= k) c = decode_store(L, wb, start, seg1, total_bits, T, P, o.pos + O, o.pos, o.cap, raw);
+            wave_sync();
+            const uint64_t evm2 = __ballot(lane <= k && c.ev != EV_NONE);
+            const unsigned ke = first_lane(evm2);
+            const unsigned kl = ke < WAVE ? ke : k;
+            const uint32_t round_bytes = __shfl(O + c.bytes, kl);
+            const uint32_t round_toks = __shfl(P + c.n, kl);
+            const uint32_t kev = ke < WAVE ? __shfl(c.ev, kl) : (uint32_t)EV_NONE;
+            const uint32_t kerr = __shfl(c.err, kl);
+            const uint32_t kexit = __shfl(c.exit, kl);
+            PROF_LAP(4);
+            expand_round(L, o, round_bytes);
+            PROF_LAP(5);
+            if (round_toks) est16 = ((kexit - S) << 4) / round_toks;
+            if (est16 < 16) est16 = 16;
+            shrink = 0;
+            switch (kev) {
+            case EV_NONE:
+                pos = kexit;
+                break;
+            case EV_EOB:
+                pos = kexit;
+                block_end = true;
+                break;
+            case EV_ERROR:
+                st = (int32_t)kerr;
+                stop = true;
+                break;
+            case EV_STARVED:
+                stop = true;
+                break;
+            default:   // EV_FULL / EV_PARTIAL
+                st = full_status;
+                stop = true;
+                break;
             }
-            // a full buffer stops the reference before its distance check
-            // (ipp:475-476) when the caller's capacity is exact (raw); the
-            // pmd driver gives it one spare byte, so the check comes first
-            if (raw && o.pos >= o.cap) break;
-            if (dist > o.pos) { st = ST_INVALID_DISTANCE; break; }
-            if (o.pos >= o.cap) { st = full_status; break; }
-            bool overflow = false;
-            if (o.pos + len > o.cap) { len = o.cap - o.pos; overflow = true; }
-            stage_room(o, len);
-            copy_match(o, len, dist);
-            if (overflow) { st = full_status; break; }
         }
-        if (!block_end) break;   // starved, error or overflow
+        if (stop) break;
+        PROF_MARK();
     }
-    if (o.pos > o.base) flush_stage(o, o.pos);
+    PROF_MARK();
+    ring_flush(L, o, o.flushed, o.pos);
+    PROF_LAP(12);
+    PROF_FLUSH();
     out_len = o.pos;
     status = st;
 }
 
-__global__ void __launch_bounds__(WAVES_PER_BLOCK * WAVE)
-inflate_kernel_v1(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
-                  const uint32_t* __restrict__ in_len, uint32_t n_msgs, uint8_t* __restrict__ out,
-                  const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
-                  uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t raw)
+__global__ void __launch_bounds__(WAVE)
+inflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+               const uint32_t* __restrict__ in_len, uint32_t n_msgs, uint8_t* __restrict__ out,
+               const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
+               uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t raw)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const unsigned wave = threadIdx.x / WAVE;
-    WaveLds& L = reinterpret_cast<WaveLds*>(smem)[wave];
-    const uint32_t msg = blockIdx.x * WAVES_PER_BLOCK + wave;
-    if (msg >= n_msgs) return;
-    InMsg m;
-    m.p = in + in_off[msg];
-    m.n = in_len[msg];
-    m.total = m.n + (raw ? 0u : 4u);
-    Out o;
-    o.g = out + out_off[msg];
-    o.cap = out_cap[msg];
-    o.pos = 0;
-    o.base = 0;
-    o.stage = L.stage;
-    uint32_t ol = 0;
-    int32_t st = 0;
-    inflate_one(L, m, o, ol, st, raw != 0);
-    if (lane_id() == 0) {
-        out_len[msg] = ol;
-        status[msg] = st;
+    WaveLds& L = *reinterpret_cast<WaveLds*>(smem);
+    for (uint32_t msg = blockIdx.x; msg < n_msgs; msg += gridDim.x) {
+        Msg m;
+        m.p = in + in_off[msg];
+        m.n = in_len[msg];
+        m.total = m.n + (raw ? 0u : 4u);
+        Out o;
+        o.g = out + out_off[msg];
+        o.cap = out_cap[msg];
+        o.pos = 0;
+        o.flushed = 0;
+        uint32_t ol = 0;
+        int32_t st = 0;
+        inflate_msg(L, m, o, raw != 0, ol, st);
+        if (lane_id() == 0) {
+            out_len[msg] = ol;
+            status[msg] = st;
+        }
+        wave_sync();
     }
 }
 
@@ -441,17 +698,20 @@ inflate_kernel_v1(const uint8_t* __restrict__ in, const uint64_t* __restrict__ i
 
 // ---------------------------------------------------------------- launcher
 
-extern "C" int bpmd_internal_inflate_v1(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
-                                        uint32_t n, uint8_t* out, const uint64_t* out_off,
-                                        const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
-                                        uint32_t raw, hipStream_t stream)
+extern "C" int bpmd_internal_inflate(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n,
+                                     uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                                     uint32_t* out_len, int32_t* status, uint32_t raw, hipStream_t stream)
 {
     using namespace bpmd;
     if (n == 0) return 0;
-    dim3 grid((n + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
-    size_t lds = sizeof(WaveLds) * WAVES_PER_BLOCK;
-    hipLaunchKernelGGL(inflate_kernel_v1, grid, dim3(WAVES_PER_BLOCK * WAVE), lds, stream, in, in_off, in_len, n,
-                       out, out_off, out_cap, out_len, status, raw);
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const size_t lds = sizeof(WaveLds);
+    const unsigned per_cu = (unsigned)(160 * 1024 / lds);
+    unsigned grid = (unsigned)cus * (per_cu ? per_cu : 1);
+    if (grid > n) grid = n;
+    hipLaunchKernelGGL(inflate_kernel, dim3(grid), dim3(WAVE), lds, stream, in, in_off, in_len, n, out, out_off,
+                       out_cap, out_len, status, raw);
     return (int)hipGetLastError();
 }
 
@@ -473,5 +733,20 @@ extern "C" int bpmd_internal_init_fixed(void)
     hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_fixed_lens), fl, sizeof fl);
     if (e != hipSuccess) return (int)e;
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_fixed_dists), fd, sizeof fd);
+    return (int)e;
+}
+
+// diagnostic counters (meaningful only in the -DBPMD_PROF build)
+extern "C" int bpmd_diag_counters(unsigned long long* out16, int reset)
+{
+    using namespace bpmd;
+    hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) return (int)e;
+    e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 16);
+    if (e != hipSuccess) return (int)e;
+    if (reset) {
+        unsigned long long z[16] = {0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof z);
+    }
     return (int)e;
 }

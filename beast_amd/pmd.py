@@ -44,7 +44,8 @@ def lib():
     """Load libbeast_pmd.so (building it first if this checkout has none)."""
     global _LIB
     if _LIB is None:
-        path = _build.LIB
+        # BPMD_LIB selects a diagnostic variant (e.g. libbeast_pmd_prof.so)
+        path = os.environ.get("BPMD_LIB", _build.LIB)
         if not os.path.exists(path):
             _build.build()
         L = ctypes.CDLL(path)

@@ -1,0 +1,52 @@
+"""Diagnostic: per-phase cycle counters of the inflate kernel (prof build).
+
+    python beast_amd/build.py prof
+    BPMD_LIB=beast_amd/libbeast_pmd_prof.so python scripts/diag_inflate.py
+"""
+import ctypes
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+from beast_amd import pmd, synth  # noqa: E402
+
+NAMES = {0: "total", 1: "header+tables", 2: "passA", 3: "passB+fix", 4: "scan+compact", 5: "expand",
+         6: "#rounds", 7: "#passB iters", 8: "#blocks", 9: "#ptrjump iters", 10: "window load", 11: "#window loads",
+         12: "final flush"}
+
+
+def main():
+    n = int(os.environ.get("DIAG_MSGS", "8192"))
+    kind = os.environ.get("DIAG_KIND", "json")
+    size = int(os.environ.get("DIAG_SIZE", "4096"))
+    lens = np.full(n, size, dtype=np.uint32)
+    raw, off, ln = synth.make_batch(kind, lens, seed=0x5EED0002)
+    payloads = bench.pmd_compress_host(raw, off, ln)
+    buf, coff, clen = bench.pack(payloads)
+    dev = torch.device("cuda", 0)
+    src = pmd.Batch(torch.from_numpy(buf).to(dev), torch.from_numpy(coff).to(dev), torch.from_numpy(clen).to(dev))
+    L = pmd.lib()
+    L.bpmd_diag_counters.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    c = (ctypes.c_ulonglong * 16)()
+    r = pmd.inflate_batch(src, size)
+    torch.cuda.synchronize()
+    L.bpmd_diag_counters(c, 1)
+    t0 = time.perf_counter()
+    r = pmd.inflate_batch(src, size)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    L.bpmd_diag_counters(c, 1)
+    assert int((r.status != 0).sum()) == 0
+    print(f"{n} msgs x {size} B {kind}: {dt * 1e3:.2f} ms, ratio {clen.sum() / (n * size):.3f}")
+    for i in range(13):
+        print(f"  {NAMES[i]:>16}: {c[i] / n:14.1f} per msg")
+
+
+if __name__ == "__main__":
+    main()
