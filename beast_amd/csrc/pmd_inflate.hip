@@ -62,6 +62,7 @@ struct alignas(16) WaveLds {
         struct {
             WaveTableScratch ts;
             uint8_t lens[320];
+            alignas(4) uint8_t runval[320];   // code-length run starts: value + 1
         } h;
     } u;
     uint16_t tab[kEnough];
@@ -71,13 +72,14 @@ __device__ uint16_t g_fixed_lens[512];
 __device__ uint16_t g_fixed_dists[32];
 
 // Diagnostic build only (-DBPMD_PROF): per-phase cycle and event counters.
-__device__ unsigned long long g_prof[16];
+__device__ unsigned long long g_prof[24];
+__device__ unsigned long long g_prof_dbg[16];
 #ifdef BPMD_PROF
-#define PROF_DECL unsigned long long prof_[16] = {0}; unsigned long long prof_t_ = __builtin_amdgcn_s_memtime()
+#define PROF_DECL unsigned long long prof_[24] = {0}; unsigned long long prof_t_ = __builtin_amdgcn_s_memtime()
 #define PROF_MARK() (prof_t_ = __builtin_amdgcn_s_memtime())
 #define PROF_LAP(i) do { unsigned long long t2_ = __builtin_amdgcn_s_memtime(); prof_[i] += t2_ - prof_t_; prof_t_ = t2_; } while (0)
 #define PROF_CNT(i, n) (prof_[i] += (n))
-#define PROF_FLUSH() do { if (lane_id() == 0) for (int i_ = 0; i_ < 16; ++i_) atomicAdd(&g_prof[i_], prof_[i_]); } while (0)
+#define PROF_FLUSH() do { if (lane_id() == 0) for (int i_ = 0; i_ < 24; ++i_) atomicAdd(&g_prof[i_], prof_[i_]); } while (0)
 #else
 #define PROF_DECL
 #define PROF_MARK()
@@ -110,6 +112,36 @@ __device__ __forceinline__ uint32_t in_word(const Msg& m, uint32_t i)
         return (uint32_t)(v >> sh);
     }
     return in_byte(m, i) | (in_byte(m, i + 1) << 8) | (in_byte(m, i + 2) << 16) | (in_byte(m, i + 3) << 24);
+}
+
+// Fill the LDS window with stream bytes [wbase, wbase + IN_CAP + IN_PAD).
+// Every global load is issued before the first LDS store so their latencies
+// overlap; only the word holding the payload's end and the tail past it take
+// the byte path.
+template <unsigned NW>
+__device__ __forceinline__ void load_window(uint32_t* win, const Msg& m, uint32_t wbase)
+{
+    const unsigned lane = lane_id();
+    constexpr unsigned PER_LANE = (NW + WAVE - 1) / WAVE;
+    const uint32_t full = m.n >> 2;   // whole payload words
+    const uint32_t w0 = wbase >> 2;
+    uint32_t nfast = 0;               // window words served by plain loads
+    if ((((uintptr_t)m.p) & 3) == 0 && full > w0) {
+        nfast = full - w0 < NW ? full - w0 : NW;
+        const uint32_t* p32 = (const uint32_t*)m.p + w0;
+        uint32_t vals[PER_LANE];
+#pragma unroll
+        for (unsigned k = 0; k < PER_LANE; ++k) {
+            const uint32_t i = lane + k * WAVE;
+            vals[k] = p32[i < nfast ? i : 0];
+        }
+#pragma unroll
+        for (unsigned k = 0; k < PER_LANE; ++k) {
+            const uint32_t i = lane + k * WAVE;
+            if (i < nfast) win[i] = vals[k];
+        }
+    }
+    for (uint32_t i = nfast + lane; i < NW; i += WAVE) win[i] = in_word(m, wbase + 4 * i);
 }
 
 // 64 stream bits starting at bit p_rel of the LDS window
@@ -210,8 +242,18 @@ __device__ __forceinline__ Tok decode_tok(uint64_t v, uint32_t avail, const uint
 }
 
 struct LaneRes {
-    uint32_t exit, n, bytes, ev, err;
+    uint32_t exit, n, bytes, ev, err, trips;
 };
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t x)
+{
+#pragma unroll
+    for (unsigned d = 1; d < WAVE; d <<= 1) {
+        const uint32_t y = __shfl_xor(x, d);
+        x = x > y ? x : y;
+    }
+    return x;
+}
 
 struct Tables {
     const uint16_t* ltab;
@@ -229,8 +271,10 @@ __device__ __forceinline__ LaneRes decode_count(const WaveLds& L, uint32_t wb, u
     r.bytes = 0;
     r.ev = EV_NONE;
     r.err = 0;
+    r.trips = 0;
     uint32_t p = start;
     while (p < end) {
+        r.trips += 1;
         const uint64_t v = peek64(L.win, p - wb);
         const uint32_t avail = p < total_bits ? total_bits - p : 0;
         const Tok t = decode_tok(v, avail, T.ltab, T.lroot, T.dtab, T.droot);
@@ -262,8 +306,10 @@ __device__ __forceinline__ LaneRes decode_store(WaveLds& L, uint32_t wb, uint32_
     r.bytes = 0;
     r.ev = EV_NONE;
     r.err = 0;
+    r.trips = 0;
     uint32_t p = start;
     while (p < end) {
+        r.trips += 1;
         const uint64_t v = peek64(L.win, p - wb);
         const uint32_t avail = p < total_bits ? total_bits - p : 0;
         const Tok t = decode_tok(v, avail, T.ltab, T.lroot, T.dtab, T.droot);
@@ -412,7 +458,7 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
     }
     PROF_DECL;
     uint32_t wbase = 0;   // window start, bytes (multiple of 4)
-    for (uint32_t i = lane; i < WIN_WORDS; i += WAVE) L.win[i] = in_word(m, 4 * i);
+    load_window<WIN_WORDS>(L.win, m, 0);
     wave_sync();
     PROF_LAP(10);
     auto ensure = [&](uint32_t p, uint32_t nbytes) {
@@ -421,7 +467,7 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
             PROF_MARK();
             wbase = b0 & ~3u;
             wave_sync();
-            for (uint32_t i = lane; i < WIN_WORDS; i += WAVE) L.win[i] = in_word(m, wbase + 4 * i);
+            load_window<WIN_WORDS>(L.win, m, wbase);
             wave_sync();
             PROF_LAP(10);
             PROF_CNT(11, 1);
@@ -499,52 +545,97 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
             pos += 3 * ncode;
             wave_sync();
             unsigned croot = 0, cused = 0, cmin = 0;
+            PROF_LAP(20);
             int r = build_table_wave<BUILD_CODES>(L.u.h.lens, 19, L.tab, 7, L.u.h.ts, croot, cused, cmin);
             wave_sync();
+            PROF_LAP(16);
             if (r) { st = r; break; }
+            // code lengths (ipp:264-327): every lane decodes a code-length
+            // symbol at its own bit offset of a 64-bit window; a scalar walk
+            // then follows the true chain through the window, applying the
+            // reference's checks in order, and marks run starts; a final
+            // fill-forward expands the runs.
             bool starved = false;
-            unsigned have = 0;
-            while (have < nlen + ndist) {
-                if (total_bits - pos < croot) { starved = true; break; }
-                const uint16_t s = L.tab[ubits(pos, croot)];
-                const unsigned sym = slot_val(s);
-                const unsigned cb = slot_bits(s);
-                if (sym < 16) {
-                    pos += cb;
-                    if (lane == 0) L.u.h.lens[have] = (uint8_t)sym;
-                    ++have;
-                    continue;
+            const unsigned want = nlen + ndist;
+            for (unsigned i = lane; i < 80; i += WAVE) ((uint32_t*)L.u.h.runval)[i] = 0;
+            wave_sync();
+            unsigned have = 0, prevlen = 0;
+            while (have < want) {
+                const uint32_t w = pos;
+                const uint64_t v = peek64(L.win, w + lane - wbase * 8);
+                const uint16_t s = L.tab[lowbits(v, croot)];
+                const unsigned sym = slot_val(s), cb = slot_bits(s);
+                const unsigned xb = sym < 16 ? 0u : (sym == 16 ? 2u : sym == 17 ? 3u : 7u);
+                const unsigned x = lowbits(v >> cb, xb);
+                const uint32_t packed = (cb + xb) | (sym << 5) | (x << 10) | (cb << 17);
+                uint32_t cur = w;
+                // run starts found in this window: (position << 8) | (value + 1),
+                // collected in lane order with v_writelane, stored once
+                uint32_t marks = 0;
+                unsigned nmarks = 0;
+                while (cur < w + WAVE && have < want) {
+                    const uint32_t pk = __builtin_amdgcn_readlane(packed, cur - w);
+                    const unsigned tb = pk & 31, sy = (pk >> 5) & 31, xx = (pk >> 10) & 127, c0 = (pk >> 17) & 15;
+                    const uint32_t av = total_bits - cur;
+                    if (av < croot) { starved = true; break; }
+                    unsigned rep, val;
+                    if (sy < 16) {
+                        rep = 1;
+                        val = sy;
+                        cur += c0;
+                    } else {
+                        // code and extra bits are asked for together (ipp:282-312)
+                        if (av < tb) { starved = true; break; }
+                        if (sy == 16) {
+                            if (have == 0) { st = ST_INVALID_BIT_LENGTH_REPEAT; break; }
+                            rep = 3 + xx;
+                            val = prevlen;
+                        } else {
+                            rep = (sy == 17 ? 3 : 11) + xx;
+                            val = 0;
+                        }
+                        if (have + rep > want) { st = ST_INVALID_BIT_LENGTH_REPEAT; break; }
+                        cur += tb;
+                    }
+                    marks = lane == nmarks ? ((have << 8) | (val + 1)) : marks;
+                    ++nmarks;
+                    have += rep;
+                    prevlen = val;
                 }
-                // the reference asks for code + extra bits together (ipp:282-312)
-                const unsigned xb = sym == 16 ? 2 : sym == 17 ? 3 : 7;
-                if (total_bits - pos < cb + xb) { starved = true; break; }
-                const uint32_t x = ubits(pos + cb, xb);
-                pos += cb + xb;
-                unsigned rep, val = 0;
-                if (sym == 16) {
-                    if (have == 0) { st = ST_INVALID_BIT_LENGTH_REPEAT; break; }
-                    rep = 3 + x;
-                    wave_sync();
-                    val = L.u.h.lens[have - 1];
-                } else {
-                    rep = (sym == 17 ? 3 : 11) + x;
-                }
-                if (have + rep > nlen + ndist) { st = ST_INVALID_BIT_LENGTH_REPEAT; break; }
-                for (unsigned k = lane; k < rep; k += WAVE) L.u.h.lens[have + k] = (uint8_t)val;
-                have += rep;
-                wave_sync();
+                if (lane < nmarks) L.u.h.runval[marks >> 8] = (uint8_t)(marks & 0xff);
+                pos = cur;
+                if (st || starved) break;
             }
             if (st) break;
             if (starved) break;
             wave_sync();
+            {
+                uint32_t carry = 0;
+                const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+                for (unsigned c0 = 0; c0 < want; c0 += WAVE) {
+                    const unsigned i = c0 + lane;
+                    const uint32_t mk = i < want ? L.u.h.runval[i] : 0u;
+                    const uint64_t mask = __ballot(mk != 0);
+                    const uint64_t le = mask & upto;
+                    const unsigned j = le ? 63u - (unsigned)__builtin_clzll(le) : 0u;
+                    const uint32_t fromj = __shfl(mk, j);
+                    const uint32_t val = le ? fromj : carry;
+                    if (i < want) L.u.h.lens[i] = (uint8_t)(val - 1);
+                    if (mask) carry = __shfl(mk, 63u - (unsigned)__builtin_clzll(mask));
+                }
+            }
+            wave_sync();
+            PROF_LAP(17);
             if (L.u.h.lens[256] == 0) { st = ST_MISSING_EOB; break; }
             unsigned lroot = 0, lused = 0, lmin = 0, droot = 0, dused = 0, dmin = 0;
             r = build_table_wave<BUILD_LENS>(L.u.h.lens, nlen, L.tab, 9, L.u.h.ts, lroot, lused, lmin);
             wave_sync();
+            PROF_LAP(18);
             if (r) { st = r; break; }
             r = build_table_wave<BUILD_DISTS>(L.u.h.lens + nlen, ndist, L.tab + lused, 6, L.u.h.ts, droot, dused,
                                               dmin);
             wave_sync();
+            PROF_LAP(19);
             if (r) { st = r; break; }
             T.lroot = lroot;
             T.droot = droot;
@@ -563,11 +654,14 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
             PROF_CNT(6, 1);
             const uint32_t S = pos;
             const uint32_t rem = total_bits > S ? total_bits - S : 0;
+            // segments keep ~SEG_TOKENS tokens even when the block is short:
+            // shorter ones would rarely re-synchronise; lanes past the end of
+            // the input simply starve
             uint32_t Lseg = (SEG_TOKENS * est16) >> 4;
             if (Lseg > SEG_MAX_BITS) Lseg = SEG_MAX_BITS;
             Lseg >>= shrink;
-            if ((uint64_t)Lseg * WAVE > rem) Lseg = (rem + WAVE - 1) / WAVE;
             if (Lseg == 0) Lseg = 1;
+            (void)rem;
             ensure(S, (WAVE * Lseg + 160) / 8 + 16);
             const uint32_t wb = wbase * 8;
             const uint32_t seg0 = S + lane * Lseg, seg1 = seg0 + Lseg;
@@ -575,8 +669,23 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
             PROF_MARK();
             const LaneRes a = decode_count(L, wb, seg0, seg1, total_bits, T);
             PROF_LAP(2);
-            uint32_t start = lane == 0 ? S : from_prev_lane(a.exit);
+            PROF_CNT(13, wave_max(a.trips));
+            // cross-lane reads with every lane active (a ternary would run
+            // the permute with lane 0 switched off and read 0 from it)
+            const uint32_t a_prev = from_prev_lane(a.exit);
+            uint32_t start = lane == 0 ? S : a_prev;
             LaneRes b = decode_count(L, wb, start, seg1, total_bits, T);
+            PROF_CNT(14, wave_max(b.trips));
+#ifdef BPMD_PROF
+            if (b.trips > 200 && g_prof_dbg[0] == 0) {
+                if (atomicCAS((unsigned long long*)&g_prof_dbg[0], 0ull, 2ull) == 0ull) {
+                    g_prof_dbg[1] = lane; g_prof_dbg[2] = start; g_prof_dbg[3] = seg1; g_prof_dbg[4] = S;
+                    g_prof_dbg[5] = Lseg; g_prof_dbg[6] = b.trips; g_prof_dbg[7] = b.ev; g_prof_dbg[8] = b.exit;
+                    g_prof_dbg[9] = total_bits; g_prof_dbg[10] = a.exit; g_prof_dbg[11] = a.trips; g_prof_dbg[12] = b.n;
+                    g_prof_dbg[13] = T.lroot; g_prof_dbg[14] = T.droot; g_prof_dbg[15] = est16;
+                }
+            }
+#endif
             unsigned k;   // last lane of the round
             for (;;) {
                 PROF_CNT(7, 1);
@@ -593,6 +702,17 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
                     start = prev_exit;
                     b = decode_count(L, wb, start, seg1, total_bits, T);
                 }
+                PROF_CNT(14, wave_max(bad ? b.trips : 0u));
+#ifdef BPMD_PROF
+                if (bad && b.trips > 200 && g_prof_dbg[0] == 0) {
+                    if (atomicCAS((unsigned long long*)&g_prof_dbg[0], 0ull, 1ull) == 0ull) {
+                        g_prof_dbg[1] = lane; g_prof_dbg[2] = start; g_prof_dbg[3] = seg1; g_prof_dbg[4] = S;
+                        g_prof_dbg[5] = Lseg; g_prof_dbg[6] = b.trips; g_prof_dbg[7] = b.ev; g_prof_dbg[8] = b.exit;
+                        g_prof_dbg[9] = total_bits; g_prof_dbg[10] = fe; g_prof_dbg[11] = fb; g_prof_dbg[12] = b.n;
+                        g_prof_dbg[13] = T.lroot; g_prof_dbg[14] = T.droot; g_prof_dbg[15] = est16;
+                    }
+                }
+#endif
             }
             PROF_LAP(3);
             // token and byte offsets within the round; keep the round within
@@ -617,6 +737,7 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
             c.bytes = 0;
             c.ev = EV_NONE;
             c.err = 0;
+            c.trips = 0;
             if (lane <= k) c = decode_store(L, wb, start, seg1, total_bits, T, P, o.pos + O, o.pos, o.cap, raw);
             wave_sync();
             const uint64_t evm2 = __ballot(lane <= k && c.ev != EV_NONE);
@@ -628,6 +749,7 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
             const uint32_t kerr = __shfl(c.err, kl);
             const uint32_t kexit = __shfl(c.exit, kl);
             PROF_LAP(4);
+            PROF_CNT(15, wave_max(c.trips));
             expand_round(L, o, round_bytes);
             PROF_LAP(5);
             if (round_toks) est16 = ((kexit - S) << 4) / round_toks;
@@ -742,10 +864,12 @@ extern "C" int bpmd_diag_counters(unsigned long long* out16, int reset)
     using namespace bpmd;
     hipError_t e = hipDeviceSynchronize();
     if (e != hipSuccess) return (int)e;
-    e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 16);
+    // (the C++ overload takes the symbol by reference: pass the variable itself)
+    if (reset == 2) return (int)hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_prof_dbg), sizeof(unsigned long long) * 16);
+    e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 24);
     if (e != hipSuccess) return (int)e;
     if (reset) {
-        unsigned long long z[16] = {0};
+        unsigned long long z[24] = {0};
         e = hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof z);
     }
     return (int)e;

@@ -16,9 +16,10 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 from beast_amd import pmd, synth  # noqa: E402
 
-NAMES = {0: "total", 1: "header+tables", 2: "passA", 3: "passB+fix", 4: "scan+compact", 5: "expand",
+NAMES = {0: "-", 1: "fixed/other hdr", 2: "passA", 3: "passB+fix", 4: "scan+passC", 5: "expand",
          6: "#rounds", 7: "#passB iters", 8: "#blocks", 9: "#ptrjump iters", 10: "window load", 11: "#window loads",
-         12: "final flush"}
+         12: "final flush", 13: "passA trips", 14: "passB trips", 15: "passC trips", 16: "clen table",
+         17: "clen decode", 18: "lens table", 19: "dists table", 20: "hdr fields", 21: "-", 22: "-", 23: "-"}
 
 
 def main():
@@ -33,10 +34,10 @@ def main():
     src = pmd.Batch(torch.from_numpy(buf).to(dev), torch.from_numpy(coff).to(dev), torch.from_numpy(clen).to(dev))
     L = pmd.lib()
     L.bpmd_diag_counters.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    c = (ctypes.c_ulonglong * 16)()
+    c = (ctypes.c_ulonglong * 24)()
     r = pmd.inflate_batch(src, size)
     torch.cuda.synchronize()
-    L.bpmd_diag_counters(c, 1)
+    print("reset rc", L.bpmd_diag_counters(c, 1), flush=True)
     t0 = time.perf_counter()
     r = pmd.inflate_batch(src, size)
     torch.cuda.synchronize()
@@ -44,8 +45,13 @@ def main():
     L.bpmd_diag_counters(c, 1)
     assert int((r.status != 0).sum()) == 0
     print(f"{n} msgs x {size} B {kind}: {dt * 1e3:.2f} ms, ratio {clen.sum() / (n * size):.3f}")
-    for i in range(13):
-        print(f"  {NAMES[i]:>16}: {c[i] / n:14.1f} per msg")
+    tot = 0
+    for i in range(24):
+        if NAMES[i] != "-":
+            print(f"  {NAMES[i]:>16}: {c[i] / n:14.1f} per msg")
+    d = (ctypes.c_ulonglong * 24)()
+    L.bpmd_diag_counters(d, 2)
+    print("debug record:", list(d)[:16])
 
 
 if __name__ == "__main__":
