@@ -89,6 +89,26 @@ def cpu_baseline(comp_buf, comp_off, comp_len, raw_lens, threads, budget_s=12.0)
                       f"{threads} threads, median of 3"}
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3
+    PMC summary (profiles/rNN_*_pmc.csv, collected by scripts/profile.sh on
+    this exact workload).  FETCH_SIZE is doubled and both counters are
+    read in KiB, per MI355X_MICROARCH.md's gfx950 notes.  None if absent."""
+    import csv
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.csv")))
+    for f in reversed(files):
+        fetch, write = [], []
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                if kernel not in r["kernel"]:
+                    continue
+                (fetch if r["counter"] == "FETCH_SIZE" else write).append(float(r["value_kB"]))
+        if fetch and write:
+            return int((2 * float(np.median(fetch)) + float(np.median(write))) * 1024), os.path.relpath(f, ROOT)
+    return None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -162,6 +182,7 @@ def main():
     value = total_uncomp / (1 << 30) / (wall / args.steps)
     alg_bytes = comp + uncomp + 16 * n
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic("inflate_kernel") if n == N_MSGS else (None, None)
     result = {
         "metric": "GiB/s device-resident inflate+deflate over batched WS payloads, 1/2/4/8 GPU",
         "value": round(value, 3),
@@ -180,7 +201,8 @@ def main():
                    "parallelism": f"dp{world} (independent message shards)"},
         "parity_ok": bool(ok),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "kernel": "inflate_kernel", "kernel_ms": round(kern_ms, 4),
                      "alg_bytes_per_launch": alg_bytes},
     }
