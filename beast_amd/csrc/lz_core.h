@@ -1,0 +1,242 @@
+// lz_core.h -- encoder pieces shared by the HIP deflate kernel and the host
+// model used to size its parameters (scripts/deflate_model.cpp).
+//
+// Everything here is plain integer code callable from host or device.  The
+// encoder is NOT required to be bit-identical to Beast (the contract is a
+// byte-identical round trip and a stated size tolerance), but the pieces
+// follow the reference's design so ratios stay comparable:
+//   level table (good/lazy/nice/chain, greedy vs lazy)   zlib/detail/deflate_stream.hpp:571-590
+//   longest_match chain walk rules                       zlib/detail/deflate_stream.ipp:1747-1844
+//   lazy evaluation (f_slow) incl. TOO_FAR / filtered     deflate_stream.ipp:2045-2184
+//   length / distance codes and extra bits               deflate_stream.ipp:143-225 (get_lut)
+//   code-length run-length coding (16/17/18)             deflate_stream.ipp:978-1110
+//   block type choice (stored / fixed / dynamic)         deflate_stream.ipp:1425-1518
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define LZ_HD __host__ __device__ __forceinline__
+#else
+#define LZ_HD static inline
+#endif
+
+namespace lz {
+
+enum : int {
+    MIN_MATCH = 3, MAX_MATCH = 258, TOO_FAR = 4096, LOOKAHEAD_MIN = MAX_MATCH + MIN_MATCH + 1,
+    N_LIT = 256, EOB = 256, N_LCODES = 286, N_DCODES = 30, N_BLCODES = 19, MAX_BITS = 15, MAX_BL_BITS = 7,
+};
+
+enum Parser : int { P_STORED = 0, P_FAST = 1, P_SLOW = 2 };
+
+struct Level { uint16_t good, lazy, nice, chain; int parser; };
+
+// deflate_stream.hpp:571-590 (values of the reference's configuration table)
+LZ_HD Level level_params(int level)
+{
+    switch (level) {
+    case 0: return {0, 0, 0, 0, P_STORED};
+    case 1: return {4, 4, 8, 4, P_FAST};
+    case 2: return {4, 5, 16, 8, P_FAST};
+    case 3: return {4, 6, 32, 32, P_FAST};
+    case 4: return {4, 4, 16, 16, P_SLOW};
+    case 5: return {8, 16, 32, 32, P_SLOW};
+    case 7: return {8, 32, 128, 256, P_SLOW};
+    case 8: return {32, 128, 258, 1024, P_SLOW};
+    case 9: return {32, 258, 258, 4096, P_SLOW};
+    default: return {8, 16, 128, 128, P_SLOW};   // 6 (and -1 = default)
+    }
+}
+
+LZ_HD int ilog2(uint32_t v) { return 31 - __builtin_clz(v); }
+
+// Length symbol (257..285), its extra-bit count and extra value for a match
+// length 3..258.
+LZ_HD void len_code(unsigned len, unsigned& sym, unsigned& nx, unsigned& xv)
+{
+    unsigned l = len - MIN_MATCH;
+    if (l < 8) { sym = 257 + l; nx = 0; xv = 0; return; }
+    if (len == MAX_MATCH) { sym = 285; nx = 0; xv = 0; return; }
+    unsigned eb = (unsigned)ilog2(l) - 2;
+    unsigned hi = (l >> eb) & 3;
+    sym = 257 + 4 * (eb + 1) + hi;
+    nx = eb;
+    xv = l - ((4 | hi) << eb);
+}
+
+// Distance symbol (0..29), extra-bit count and extra value for 1..32768.
+LZ_HD void dist_code(unsigned dist, unsigned& sym, unsigned& nx, unsigned& xv)
+{
+    unsigned d = dist - 1;
+    if (d < 4) { sym = d; nx = 0; xv = 0; return; }
+    unsigned eb = (unsigned)ilog2(d) - 1;
+    unsigned hi = (d >> eb) & 1;
+    sym = 2 * (eb + 1) + hi;
+    nx = eb;
+    xv = d - ((2 | hi) << eb);
+}
+
+LZ_HD unsigned len_extra_bits(unsigned sym) { return (sym >= 265 && sym < 285) ? (sym - 261) / 4 : 0; }
+LZ_HD unsigned dist_extra_bits(unsigned sym) { return sym >= 4 ? (sym - 2) / 2 : 0; }
+
+// Fixed-Huffman code lengths (RFC 1951 §3.2.6).
+LZ_HD unsigned fixed_lit_len(unsigned sym) { return sym < 144 ? 8 : sym < 256 ? 9 : sym < 280 ? 7 : 8; }
+
+LZ_HD uint32_t reverse_bits(uint32_t code, unsigned len)
+{
+#if defined(__clang__)
+    return __builtin_bitreverse32(code) >> (32 - len);
+#else
+    uint32_t r = 0;
+    for (unsigned i = 0; i < len; ++i, code >>= 1) r = (r << 1) | (code & 1);
+    return r;
+#endif
+}
+
+// Hash of the 3 bytes at a position (bytes packed little-endian in `w`).
+LZ_HD uint32_t hash3(uint32_t w, unsigned hbits) { return ((w & 0xFFFFFFu) * 0x9E3779B1u) >> (32 - hbits); }
+
+// ---------------------------------------------------------------- Huffman
+//
+// Code lengths for one alphabet.  Deterministic restatement of the
+// two-queue Huffman construction over leaves sorted by (freq, symbol), with
+// the reference's length-limiting rule (deflate_stream.ipp:786-873): leaves
+// deeper than max_bits are clamped, the Kraft overflow is repaid by moving
+// leaves down from the deepest non-full level, and lengths are reassigned in
+// frequency order (least frequent gets the longest code).  As in the
+// reference, an alphabet with fewer than two used symbols gets dummy
+// symbols so that a complete code always exists.
+//
+// Host reference version (serial); the kernel has a wave-parallel sort and
+// runs the linear merge on one lane with identical results.
+struct HuffScratch {
+    uint32_t key[N_LCODES + 2];      // (freq << 9) | sym, sorted ascending
+    uint32_t iw[N_LCODES + 2];       // internal node weights
+    uint16_t parent[2 * N_LCODES + 4];
+    uint8_t depth[2 * N_LCODES + 4];
+};
+
+#if !defined(__HIP_DEVICE_COMPILE__)
+static inline void sort_u32(uint32_t* a, int n)
+{
+    for (int i = 1; i < n; ++i) {
+        uint32_t v = a[i];
+        int j = i - 1;
+        while (j >= 0 && a[j] > v) { a[j + 1] = a[j]; --j; }
+        a[j + 1] = v;
+    }
+}
+
+// freq[0..n) -> lens[0..n); returns the number of used symbols after dummies.
+static inline int huff_lengths_host(const uint32_t* freq, int n, int max_bits, uint8_t* lens, HuffScratch& S)
+{
+    int m = 0;
+    uint32_t f2[N_LCODES + 2];
+    for (int i = 0; i < n; ++i) { f2[i] = freq[i]; lens[i] = 0; }
+    int used = 0;
+    for (int i = 0; i < n; ++i) used += f2[i] != 0;
+    // the reference forces at least two codes (deflate_stream.ipp:911-925):
+    // dummy symbols 0 and 1 (or the first unused) with frequency 1
+    for (int i = 0; used < 2 && i < n; ++i)
+        if (f2[i] == 0) { f2[i] = 1; ++used; }
+    for (int i = 0; i < n; ++i)
+        if (f2[i]) S.key[m++] = (f2[i] << 9) | (uint32_t)i;
+    sort_u32(S.key, m);
+    // two-queue merge: leaves 0..m-1, internal nodes m..2m-2
+    int li = 0, ii = 0;
+    for (int k = 0; k < m - 1; ++k) {
+        uint32_t w[2];
+        int id[2];
+        for (int t = 0; t < 2; ++t) {
+            bool take_leaf = li < m && (ii >= k || (S.key[li] >> 9) <= S.iw[ii]);
+            if (take_leaf) { w[t] = S.key[li] >> 9; id[t] = li++; }
+            else { w[t] = S.iw[ii]; id[t] = m + ii++; }
+        }
+        S.iw[k] = w[0] + w[1];
+        S.parent[id[0]] = S.parent[id[1]] = (uint16_t)(m + k);
+    }
+    // depths top-down (root = m + m - 2)
+    int root = 2 * m - 2;
+    S.depth[root] = 0;
+    for (int v = root - 1; v >= 0; --v) S.depth[v] = (uint8_t)(S.depth[S.parent[v]] + 1);
+    // clamp + overflow repair (reference: gen_bitlen)
+    unsigned bl_count[MAX_BITS + 2] = {0};
+    int overflow = 0;
+    for (int i = 0; i < m; ++i) {
+        int d = S.depth[i];
+        if (d > max_bits) { d = max_bits; ++overflow; }
+        bl_count[d]++;
+    }
+    if (overflow) {
+        do {
+            int bits = max_bits - 1;
+            while (bl_count[bits] == 0) --bits;
+            bl_count[bits]--;
+            bl_count[bits + 1] += 2;
+            bl_count[max_bits]--;
+            overflow -= 2;
+        } while (overflow > 0);
+        // reassign: most frequent leaves (end of the sorted list) get the
+        // shortest lengths
+        int i = m - 1;
+        for (int bits = 1; bits <= max_bits; ++bits)
+            for (unsigned c = 0; c < bl_count[bits]; ++c) S.depth[i--] = (uint8_t)bits;
+    }
+    for (int i = 0; i < m; ++i) lens[S.key[i] & 511] = S.depth[i];
+    return m;
+}
+
+// Canonical codes (bit-reversed for LSB-first emission), deflate_stream.ipp:115-141.
+static inline void canonical_codes_host(const uint8_t* lens, int n, uint16_t* codes)
+{
+    unsigned cnt[MAX_BITS + 1] = {0}, next[MAX_BITS + 1];
+    for (int i = 0; i < n; ++i) cnt[lens[i]]++;
+    cnt[0] = 0;
+    unsigned code = 0;
+    for (int b = 1; b <= MAX_BITS; ++b) { code = (code + cnt[b - 1]) << 1; next[b] = code; }
+    for (int i = 0; i < n; ++i) codes[i] = lens[i] ? (uint16_t)reverse_bits(next[lens[i]]++, lens[i]) : 0;
+}
+#endif
+
+// Run-length coding of a code-length sequence (16: repeat previous 3-6,
+// 17: zeros 3-10, 18: zeros 11-138), the reference's scan_tree/send_tree
+// state machine (deflate_stream.ipp:978-1110).  `emit(sym, extra_bits,
+// extra_value)` is called per code-length symbol.  `nextlen` past the end is
+// a sentinel that never matches.
+template <class Get, class Emit>
+LZ_HD void rle_lengths(Get get, int count_n, Emit emit)
+{
+    int prevlen = -1, nextlen = get(0), count = 0;
+    int max_count = 7, min_count = 4;
+    if (nextlen == 0) { max_count = 138; min_count = 3; }
+    for (int i = 0; i < count_n; ++i) {
+        int curlen = nextlen;
+        nextlen = i + 1 < count_n ? get(i + 1) : 0xFFFF;
+        if (++count < max_count && curlen == nextlen) continue;
+        if (count < min_count) {
+            do { emit(curlen, 0, 0); } while (--count != 0);
+        } else if (curlen != 0) {
+            if (curlen != prevlen) { emit(curlen, 0, 0); --count; }
+            emit(16, 2, count - 3);
+        } else if (count <= 10) {
+            emit(17, 3, count - 3);
+        } else {
+            emit(18, 7, count - 11);
+        }
+        count = 0;
+        prevlen = curlen;
+        if (nextlen == 0) { max_count = 138; min_count = 3; }
+        else if (curlen == nextlen) { max_count = 6; min_count = 3; }
+        else { max_count = 7; min_count = 4; }
+    }
+}
+
+// Order in which code-length code lengths are sent (RFC 1951 §3.2.7).
+LZ_HD unsigned bl_order(unsigned i)
+{
+    const uint8_t o[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+    return o[i];
+}
+
+}  // namespace lz

@@ -12,6 +12,11 @@ extern "C" int bpmd_internal_inflate(const uint8_t* in, const uint64_t* in_off, 
                                         const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
                                         uint32_t raw, hipStream_t stream);
 
+extern "C" int bpmd_internal_deflate(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                     uint32_t n, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                                     uint32_t* out_len, int32_t* status, int level, int window_bits, int strategy,
+                                     hipStream_t stream);
+
 namespace {
 std::mutex g_init_mu;
 int g_init_device = -1;   // device whose symbols are initialised
@@ -53,5 +58,29 @@ extern "C" int bpmd_inflate_batch(const bpmd_cfg* cfg, const uint8_t* d_in, cons
     if (r) return r;
     int e = bpmd_internal_inflate(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
                                      d_status, (cfg->flags & BPMD_F_RAW) ? 1u : 0u, (hipStream_t)stream);
+    return e ? BPMD_R_HIP_ERROR : BPMD_R_OK;
+}
+
+extern "C" int bpmd_deflate_batch(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_off,
+                                  const uint32_t* d_in_len, uint32_t n_msgs, uint8_t* d_out,
+                                  const uint64_t* d_out_off, const uint32_t* d_out_cap,
+                                  uint32_t* d_out_len, int32_t* d_status, void* stream)
+{
+    if (!cfg) return BPMD_R_INVALID_ARGUMENT;
+    // deflate_stream.ipp:235-253: level -1 means 6; windowBits 8 becomes 9;
+    // anything outside level 0..9, windowBits 8..15, memLevel 1..9 throws
+    // std::invalid_argument.
+    int level = cfg->level == -1 ? 6 : cfg->level;
+    int wbits = cfg->window_bits == 8 ? 9 : cfg->window_bits;
+    if (level < 0 || level > 9 || wbits < 8 || wbits > 15 || cfg->mem_level < 1 || cfg->mem_level > 9)
+        return BPMD_R_INVALID_ARGUMENT;
+    if (cfg->strategy < BPMD_STRATEGY_NORMAL || cfg->strategy > BPMD_STRATEGY_FIXED) return BPMD_R_INVALID_ARGUMENT;
+    if (n_msgs == 0) return BPMD_R_OK;
+    if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_cap || !d_out_len || !d_status)
+        return BPMD_R_INVALID_ARGUMENT;
+    int r = bpmd_init();
+    if (r) return r;
+    int e = bpmd_internal_deflate(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
+                                  d_status, level, wbits, cfg->strategy, (hipStream_t)stream);
     return e ? BPMD_R_HIP_ERROR : BPMD_R_OK;
 }

@@ -1,0 +1,959 @@
+// pmd_deflate.hip -- batched raw-DEFLATE encode of permessage-deflate
+// messages on gfx950 (CDNA4, wave64).  One wavefront owns one message at a
+// time; messages are independent streams (no_context_takeover, a4 in
+// SURVEY.md §8).
+//
+// Output per message is what Beast's deflater emits for one message driven
+// by impl_base<true>::deflate (websocket/detail/impl_base.hpp:85-154): the
+// message's blocks with BFINAL = 0, then the header bits of Flush::sync's
+// empty stored block (000) and byte padding, with the 00 00 FF FF tail
+// stripped.  The block contents are this kernel's own parse (the contract is
+// a byte-identical round trip and a compressed-size tolerance, not
+// bit-identity with zlib); scripts/deflate_model.cpp is the host model of
+// exactly this algorithm.
+//
+// Per 4 KiB chunk of a message (small messages: one chunk, no history; large
+// messages: each chunk sees the previous 4 KiB as history):
+//   1. window -> LDS with 16-byte loads;
+//   2. hash chains: 64 positions per step; LDS exchange on a 2^11 head table
+//      links every position to the previous one with the same 3-byte hash;
+//   3. parse: the chunk is cut into 64 lane segments; each lane runs the
+//      reference's greedy (levels 1-3) or lazy (4-9) matcher with its
+//      chain / lazy / nice / good limits (deflate_stream.hpp:571-590) over
+//      its segment, writing tokens by position and a token-start bitmap;
+//   4. boundary repair: an exclusive prefix max of segment end positions
+//      gives each lane the first position it owns; tokens covered by an
+//      earlier lane's last match are dropped and a straddling token keeps
+//      its tail (a match with the same distance, or literals);
+//   5. histograms with LDS atomics, Huffman code lengths (wave bitonic
+//      sort, linear two-queue merge on one lane per tree, depths by pointer
+//      jumping, the reference's 15-bit limit repair), canonical codes;
+//   6. block choice as the reference's tr_flush_block (stored / fixed /
+//      dynamic, deflate_stream.ipp:1425-1518);
+//   7. bit packing: per-lane bit counts, wave prefix sum, ds_or into an LDS
+//      bit buffer, dword stores to the output slot.
+#include "pmd_common.h"
+#include "wave_util.h"
+#include "lz_core.h"
+
+namespace bpmd {
+namespace dfl {
+
+constexpr unsigned CHUNK = 4096;
+constexpr unsigned HB = 11;
+constexpr unsigned HSIZE = 1u << HB;
+constexpr unsigned MIN_SEG = 32;
+constexpr uint32_t NONE = 0xFFFFu;
+constexpr unsigned NODES = 576 + 64;          // lit tree nodes [0, 576), dist tree [576, 640)
+constexpr unsigned NODES_PER_LANE = NODES / WAVE;
+constexpr unsigned DIST_IDX = 288;            // dist symbol s lives at lens/codes[288 + s]
+
+struct HuffLds {
+    uint32_t lf[288];
+    uint32_t df[32];
+    uint32_t bf[20];
+    uint32_t keys[512];
+    uint16_t iw[320];            // internal node weights: lit [0, 288), dist [288, 320)
+    uint16_t parent[NODES];
+    uint8_t depth[NODES];
+    uint8_t lens[320];
+    uint32_t codes[320];         // reversed code | len << 16
+    uint32_t blcount[2][16];
+    uint8_t bll[20];
+    uint32_t blc[20];
+    uint32_t misc[8];
+};
+
+template <int HIST>
+struct alignas(16) DefLds {
+    static constexpr unsigned W = HIST + CHUNK;
+    uint32_t win[(W + 128) / 4];     // window bytes at byte offset `ws`; output bit buffer after the parse
+    union {
+        uint16_t prev[W < 4096 ? 4096 : W];
+        HuffLds h;
+    } a;
+    union {
+        uint32_t head[HSIZE];
+        uint16_t tok[CHUNK];
+    } b;
+};
+
+struct Params {
+    lz::Level L;
+    int strategy;        // bpmd_strategy
+    unsigned max_dist;   // w_size - MIN_LOOKAHEAD
+};
+
+// ------------------------------------------------------------------ window
+
+struct Win {
+    const uint32_t* w;
+    const uint8_t* b;
+    unsigned ws;
+    __device__ __forceinline__ uint32_t byte(unsigned i) const { return b[ws + i]; }
+    __device__ __forceinline__ uint32_t dw(unsigned i) const
+    {
+        const unsigned j = ws + i;
+        const uint32_t lo = w[j >> 2], hi = w[(j >> 2) + 1];
+        return __builtin_amdgcn_alignbit(hi, lo, (j & 3) * 8);
+    }
+};
+
+template <int HIST>
+__device__ __forceinline__ unsigned load_window(DefLds<HIST>& S, const uint8_t* src, unsigned nbytes)
+{
+    const uintptr_t a = (uintptr_t)src;
+    const unsigned s = (unsigned)(a & 15);
+    const uint4* g = (const uint4*)(a - s);
+    const unsigned units = (s + nbytes + 15) >> 4;
+    uint4* l = (uint4*)S.win;
+    for (unsigned u = lane_id(); u < units; u += WAVE) l[u] = g[u];
+    return s;
+}
+
+// -------------------------------------------------------------- matching
+
+__device__ __forceinline__ unsigned match_len(const Win& W, unsigned c, unsigned p, unsigned maxl)
+{
+    unsigned l = 0;
+    for (;;) {
+        const uint32_t x = W.dw(c + l) ^ W.dw(p + l);
+        if (x) { l += (unsigned)__builtin_ctz(x) >> 3; break; }
+        l += 4;
+        if (l >= maxl) break;
+    }
+    return l < maxl ? l : maxl;
+}
+
+// longest_match restated per lane (deflate_stream.ipp:1747-1844), window
+// coordinates; returns the best length (> thr) or thr.
+__device__ __forceinline__ unsigned find_match(const Win& W, const uint16_t* prev, unsigned q, unsigned end,
+                                               unsigned thr, const Params& P, unsigned& dist)
+{
+    using namespace lz;
+    if (P.strategy == 2 || q + MIN_MATCH > end) return thr;
+    const unsigned maxl = end - q < (unsigned)MAX_MATCH ? end - q : (unsigned)MAX_MATCH;
+    if (P.strategy == 3) {   // rle: distance one only (f_rle, deflate_stream.ipp:2190-2270)
+        if (q == 0) return thr;
+        const uint32_t v = W.byte(q - 1) * 0x01010101u;
+        unsigned l = 0;
+        for (;;) {
+            const uint32_t x = W.dw(q + l) ^ v;
+            if (x) { l += (unsigned)__builtin_ctz(x) >> 3; break; }
+            l += 4;
+            if (l >= maxl) break;
+        }
+        l = l < maxl ? l : maxl;
+        if (l > thr && l >= (unsigned)MIN_MATCH) { dist = 1; return l; }
+        return thr;
+    }
+    unsigned chain = P.L.chain;
+    if (thr >= P.L.good) chain >>= 2;
+    const unsigned nice = P.L.nice < maxl ? P.L.nice : maxl;
+    unsigned best = thr, bd = 0;
+    const uint32_t b0 = W.byte(q);
+    uint32_t pb = best < maxl ? W.byte(q + best) : 0;
+    uint32_t c = prev[q];
+    while (c != NONE && q - c <= P.max_dist && chain-- > 0) {
+        if (best < maxl && W.byte(c + best) == pb && W.byte(c) == b0) {
+            const unsigned l = match_len(W, c, q, maxl);
+            if (l > best) {
+                best = l;
+                bd = q - c;
+                if (l >= nice) break;
+                pb = best < maxl ? W.byte(q + best) : 0;
+            }
+        }
+        c = prev[c];
+    }
+    if (best > thr && best <= 5 && (P.strategy == 1 || (best == (unsigned)MIN_MATCH && bd > (unsigned)TOO_FAR)))
+        return thr;
+    if (best > thr) dist = bd;
+    return best;
+}
+
+// ---------------------------------------------------------------- bit sink
+
+struct BitOr {
+    uint32_t* w;
+    uint32_t wpos;
+    unsigned nb;
+    uint64_t acc;
+    __device__ __forceinline__ void start(uint32_t* words, uint32_t bitpos)
+    {
+        w = words;
+        wpos = bitpos >> 5;
+        nb = bitpos & 31;
+        acc = 0;
+    }
+    __device__ __forceinline__ void put(uint32_t v, unsigned n)
+    {
+        acc |= (uint64_t)v << nb;
+        nb += n;
+        if (nb >= 32) {
+            atomicOr(&w[wpos], (uint32_t)acc);
+            acc >>= 32;
+            nb -= 32;
+            ++wpos;
+        }
+    }
+    __device__ __forceinline__ void flush()
+    {
+        if (nb) atomicOr(&w[wpos], (uint32_t)acc);
+        nb = 0;
+        acc = 0;
+    }
+};
+
+// ------------------------------------------------------------- per-lane tokens
+
+struct LaneToks {
+    uint64_t kept;       // token starts (relative to a) owned after repair
+    unsigned a, b;       // segment [a, b) in window coordinates
+    unsigned lastdist;   // distance of a match starting at b - 1
+    unsigned rem_kind;   // 0 none, 1 match, 2 literals
+    unsigned rem_len, rem_dist, rem_b0, rem_b1;
+};
+
+// Calls f(is_match, lit_or_len, dist) for every owned token in order.
+template <class F>
+__device__ __forceinline__ void for_tokens(const LaneToks& T, const uint16_t* tok, unsigned a0, F f)
+{
+    if (T.rem_kind == 1) f(true, T.rem_len, T.rem_dist);
+    else if (T.rem_kind == 2) {
+        f(false, T.rem_b0, 0u);
+        if (T.rem_len > 1) f(false, T.rem_b1, 0u);
+    }
+    uint64_t m = T.kept;
+    while (m) {
+        const unsigned t = (unsigned)__builtin_ctzll(m);
+        m &= m - 1;
+        const unsigned pos = T.a + t;
+        const uint32_t e = tok[pos - a0];
+        if (e & 0x8000u) {
+            const unsigned d = pos + 1 < T.b ? (unsigned)tok[pos + 1 - a0] + 1 : T.lastdist;
+            f(true, (e & 0xFFu) + 3, d);
+        } else {
+            f(false, e, 0u);
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t pack_code(uint32_t code, unsigned len)
+{
+    return (len ? lz::reverse_bits(code, len) : 0u) | (len << 16);
+}
+
+// --------------------------------------------------------------- Huffman
+
+// Two-queue merge for one tree, run by one lane (lit on lane 0, dist on lane
+// 1 at the same time).  Leaves are the sorted keys [kb, kb + m); internal
+// node k is node m + k; parent[] gets node ids relative to the tree base.
+__device__ __forceinline__ void merge_tree(HuffLds& H, unsigned kb, unsigned m, unsigned ib, unsigned pb)
+{
+    unsigned li = 0, ii = 0;
+    uint32_t kw = m ? (H.keys[kb] >> 9) & 0x3FFFFFu : 0;
+    for (unsigned k = 0; k + 1 < m; ++k) {
+        uint32_t w0, w1;
+        unsigned id0, id1;
+        {
+            const uint32_t iwv = ii < k ? H.iw[ib + ii] : 0xFFFFFFFFu;
+            const bool leaf = li < m && (ii >= k || kw <= iwv);
+            if (leaf) { w0 = kw; id0 = li++; kw = li < m ? (H.keys[kb + li] >> 9) & 0x3FFFFFu : 0; }
+            else { w0 = iwv; id0 = m + ii++; }
+        }
+        {
+            const uint32_t iwv = ii < k ? H.iw[ib + ii] : 0xFFFFFFFFu;
+            const bool leaf = li < m && (ii >= k || kw <= iwv);
+            if (leaf) { w1 = kw; id1 = li++; kw = li < m ? (H.keys[kb + li] >> 9) & 0x3FFFFFu : 0; }
+            else { w1 = iwv; id1 = m + ii++; }
+        }
+        H.iw[ib + k] = (uint16_t)(w0 + w1);
+        H.parent[pb + id0] = (uint16_t)(m + k);
+        H.parent[pb + id1] = (uint16_t)(m + k);
+    }
+}
+
+// Serial build for a tiny alphabet (the code-length code, 19 symbols) on
+// lane 0, same algorithm as lz::huff_lengths_host.
+__device__ __forceinline__ void tiny_lengths(const uint32_t* freq, unsigned n, unsigned max_bits, uint8_t* lens,
+                                             uint32_t* key, uint16_t* iw, uint16_t* parent, uint8_t* depth)
+{
+    uint32_t f2[lz::N_BLCODES];
+    unsigned used = 0;
+    for (unsigned i = 0; i < n; ++i) { f2[i] = freq[i]; lens[i] = 0; used += f2[i] != 0; }
+    for (unsigned i = 0; used < 2 && i < n; ++i)
+        if (f2[i] == 0) { f2[i] = 1; ++used; }
+    unsigned m = 0;
+    for (unsigned i = 0; i < n; ++i)
+        if (f2[i]) {
+            const uint32_t v = (f2[i] << 9) | i;
+            unsigned j = m++;
+            while (j > 0 && key[j - 1] > v) { key[j] = key[j - 1]; --j; }
+            key[j] = v;
+        }
+    unsigned li = 0, ii = 0;
+    for (unsigned k = 0; k + 1 < m; ++k) {
+        uint32_t w[2];
+        unsigned id[2];
+        for (int t = 0; t < 2; ++t) {
+            const bool leaf = li < m && (ii >= k || (key[li] >> 9) <= iw[ii]);
+            if (leaf) { w[t] = key[li] >> 9; id[t] = li++; }
+            else { w[t] = iw[ii]; id[t] = m + ii++; }
+        }
+        iw[k] = (uint16_t)(w[0] + w[1]);
+        parent[id[0]] = parent[id[1]] = (uint16_t)(m + k);
+    }
+    const unsigned root = 2 * m - 2;
+    depth[root] = 0;
+    for (int v = (int)root - 1; v >= 0; --v) depth[v] = (uint8_t)(depth[parent[v]] + 1);
+    unsigned blc[16] = {0};
+    int overflow = 0;
+    for (unsigned i = 0; i < m; ++i) {
+        unsigned d = depth[i];
+        if (d > max_bits) { d = max_bits; ++overflow; }
+        blc[d]++;
+    }
+    if (overflow) {
+        do {
+            unsigned bits = max_bits - 1;
+            while (blc[bits] == 0) --bits;
+            blc[bits]--;
+            blc[bits + 1] += 2;
+            blc[max_bits]--;
+            overflow -= 2;
+        } while (overflow > 0);
+        int i = (int)m - 1;
+        for (unsigned bits = 1; bits <= max_bits; ++bits)
+            for (unsigned c = 0; c < blc[bits]; ++c) depth[i--] = (uint8_t)bits;
+    }
+    for (unsigned i = 0; i < m; ++i) lens[key[i] & 511] = depth[i];
+}
+
+// Lit/len and distance code lengths + canonical codes for the current
+// histograms (H.lf with EOB counted, H.df).  Whole wave.
+__device__ void build_trees(HuffLds& H)
+{
+    const unsigned lane = lane_id();
+    // --- keys, with the reference's "at least two codes" dummies
+    unsigned used_l = 0, used_d = 0;
+    for (unsigned i = lane; i < 320; i += WAVE) {
+        used_l += (i < 286 && H.lf[i] != 0);
+        used_d += (i >= DIST_IDX && i < DIST_IDX + 30 && H.df[i - DIST_IDX] != 0);
+    }
+    used_l = wave_sum(used_l);
+    used_d = wave_sum(used_d);
+    for (unsigned i = lane; i < 512; i += WAVE) {
+        uint32_t k = 0xFFFFFFFFu;
+        if (i < 286 && H.lf[i]) k = (H.lf[i] << 9) | i;
+        else if (i >= DIST_IDX && i < DIST_IDX + 30 && H.df[i - DIST_IDX]) k = 0x80000000u | (H.df[i - DIST_IDX] << 9) | (i - DIST_IDX);
+        H.keys[i] = k;
+    }
+    wave_sync();
+    if (lane == 0) {
+        for (unsigned i = 0; used_l < 2 && i < 286; ++i)
+            if (H.lf[i] == 0) { H.keys[i] = (1u << 9) | i; ++used_l; }
+        for (unsigned i = 0; used_d < 2 && i < 30; ++i)
+            if (H.df[i] == 0) { H.keys[DIST_IDX + i] = 0x80000000u | (1u << 9) | i; ++used_d; }
+    }
+    used_l = used_l < 2 ? 2 : used_l;
+    used_d = used_d < 2 ? 2 : used_d;
+    wave_sync();
+    // --- bitonic sort of 512 keys (4 compare-exchanges per lane per stage)
+    for (unsigned k = 2; k <= 512; k <<= 1) {
+        for (unsigned j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+            for (unsigned t = 0; t < 4; ++t) {
+                const unsigned i = lane + t * WAVE;
+                const unsigned lo = ((i / j) * 2 * j) + (i % j), hi = lo + j;
+                const uint32_t x = H.keys[lo], y = H.keys[hi];
+                const bool up = (lo & k) == 0;
+                if ((x > y) == up) { H.keys[lo] = y; H.keys[hi] = x; }
+            }
+            wave_sync();
+        }
+    }
+    const unsigned ml = used_l, md = used_d;
+    // --- merges (lane 0: lit, lane 1: dist)
+    if (lane < 2) {
+        if (lane == 0) merge_tree(H, 0, ml, 0, 0);
+        else merge_tree(H, ml, md, 288, 576);
+    }
+    wave_sync();
+    // --- depths by pointer jumping over both trees
+    const unsigned root_l = 2 * ml - 2, root_d = 576 + 2 * md - 2;
+    {
+        uint32_t anc[NODES_PER_LANE], dep[NODES_PER_LANE];
+#pragma unroll
+        for (unsigned t = 0; t < NODES_PER_LANE; ++t) {
+            const unsigned v = lane + t * WAVE;
+            const bool lit = v < 576;
+            const unsigned root = lit ? root_l : root_d;
+            const bool valid = lit ? v <= root_l : (v >= 576 && v <= root_d);
+            anc[t] = valid && v != root ? (unsigned)H.parent[v] + (lit ? 0u : 576u) : v;
+            dep[t] = valid && v != root ? 1u : 0u;
+            if (valid) {
+                H.parent[v] = (uint16_t)anc[t];
+                H.depth[v] = (uint8_t)dep[t];
+            }
+        }
+        wave_sync();
+        for (int round = 0; round < 10; ++round) {
+            bool any = false;
+#pragma unroll
+            for (unsigned t = 0; t < NODES_PER_LANE; ++t) {
+                const unsigned v = lane + t * WAVE;
+                const unsigned a = anc[t];
+                if (a != v) {
+                    const unsigned aa = H.parent[a];
+                    if (aa != a) any = true;
+                    dep[t] += H.depth[a];
+                    anc[t] = aa;
+                }
+            }
+            wave_sync();
+#pragma unroll
+            for (unsigned t = 0; t < NODES_PER_LANE; ++t) {
+                const unsigned v = lane + t * WAVE;
+                const bool lit = v < 576;
+                const bool valid = lit ? v <= root_l : (v >= 576 && v <= root_d);
+                if (valid) {
+                    H.parent[v] = (uint16_t)anc[t];
+                    H.depth[v] = (uint8_t)dep[t];
+                }
+            }
+            wave_sync();
+            if (!ballot(any)) break;
+        }
+    }
+    // --- length limit (15) and per-length counts
+    for (unsigned i = lane; i < 32; i += WAVE) H.blcount[i >> 4][i & 15] = 0;
+    wave_sync();
+    unsigned ovf_l = 0, ovf_d = 0;
+    for (unsigned i = lane; i < ml + md; i += WAVE) {
+        const bool lit = i < ml;
+        const unsigned v = lit ? i : 576 + (i - ml);
+        unsigned d = H.depth[v];
+        if (d > lz::MAX_BITS) { d = lz::MAX_BITS; if (lit) ++ovf_l; else ++ovf_d; }
+        atomicAdd(&H.blcount[lit ? 0 : 1][d], 1u);
+    }
+    ovf_l = wave_sum(ovf_l);
+    ovf_d = wave_sum(ovf_d);
+    wave_sync();
+    if (ovf_l | ovf_d) {
+        if (lane < 2) {
+            int overflow = (int)(lane == 0 ? ovf_l : ovf_d);
+            uint32_t* bc = H.blcount[lane];
+            while (overflow > 0) {
+                unsigned bits = lz::MAX_BITS - 1;
+                while (bc[bits] == 0) --bits;
+                bc[bits]--;
+                bc[bits + 1] += 2;
+                bc[lz::MAX_BITS]--;
+                overflow -= 2;
+            }
+        }
+        wave_sync();
+        // reassign: the r-th most frequent leaf gets the r-th shortest length
+        for (unsigned i = lane; i < ml + md; i += WAVE) {
+            const bool lit = i < ml;
+            if ((lit ? ovf_l : ovf_d) == 0) continue;
+            const unsigned m = lit ? ml : md, leaf = lit ? i : i - ml;
+            const unsigned r = m - 1 - leaf;
+            const uint32_t* bc = H.blcount[lit ? 0 : 1];
+            unsigned cum = 0, bits = 1;
+            for (; bits <= lz::MAX_BITS; ++bits) {
+                cum += bc[bits];
+                if (r < cum) break;
+            }
+            H.depth[lit ? leaf : 576 + leaf] = (uint8_t)bits;
+        }
+        wave_sync();
+    }
+    // --- scatter lengths to symbols
+    for (unsigned i = lane; i < 320; i += WAVE) H.lens[i] = 0;
+    wave_sync();
+    for (unsigned i = lane; i < ml + md; i += WAVE) {
+        const bool lit = i < ml;
+        const uint32_t key = H.keys[i];
+        const unsigned sym = key & 511;
+        H.lens[lit ? sym : DIST_IDX + sym] = H.depth[lit ? i : 576 + (i - ml)];
+    }
+    wave_sync();
+}
+
+// Canonical codes for lens[base, base + n) into codes[].
+__device__ __forceinline__ void canonical_codes(HuffLds& H, unsigned base, unsigned n)
+{
+    const unsigned lane = lane_id();
+    uint32_t next = 0;   // lane b (1..15) holds next_code[b]
+    {
+        // counts per length
+        uint32_t cnt = 0;
+        for (unsigned c = 0; c < n; c += WAVE) {
+            const unsigned i = c + lane;
+            const unsigned len = i < n ? H.lens[base + i] : 0;
+            for (unsigned b = 1; b <= lz::MAX_BITS; ++b) {
+                const unsigned k = (unsigned)__builtin_popcountll(ballot(len == b));
+                if (lane == b) cnt += k;
+            }
+        }
+        // next_code[b] = (next_code[b-1] + cnt[b-1]) << 1
+        uint32_t code = 0;
+        for (unsigned b = 1; b <= lz::MAX_BITS; ++b) {
+            const uint32_t cprev = __shfl(cnt, b - 1);
+            code = (code + (b == 1 ? 0u : cprev)) << 1;
+            if (lane == b) next = code;
+        }
+    }
+    for (unsigned c = 0; c < n; c += WAVE) {
+        const unsigned i = c + lane;
+        const unsigned len = i < n ? H.lens[base + i] : 0;
+        uint32_t code = 0;
+        for (unsigned b = 1; b <= lz::MAX_BITS; ++b) {
+            const uint64_t m = ballot(len == b);
+            const uint32_t nb = __shfl(next, b);
+            if (len == b) code = nb + popc_below(m);
+            if (lane == b) next += (uint32_t)__builtin_popcountll(m);
+        }
+        if (i < n) H.codes[base + i] = pack_code(code, len);
+    }
+    wave_sync();
+}
+
+__device__ __forceinline__ unsigned fixed_code(unsigned sym, unsigned& len)
+{
+    if (sym < 144) { len = 8; return 0x30 + sym; }
+    if (sym < 256) { len = 9; return 0x190 + (sym - 144); }
+    if (sym < 280) { len = 7; return sym - 256; }
+    len = 8;
+    return 0xC0 + (sym - 280);
+}
+
+// ------------------------------------------------------------------ kernel
+
+struct MsgOut {
+    uint8_t* dst;
+    uint32_t cap;
+    uint32_t opos;     // bytes completed
+    uint32_t carry;    // pending partial byte
+    unsigned cbits;    // valid bits in carry
+    bool overflow;
+};
+
+__device__ __forceinline__ void put_bytes_global(MsgOut& o, const uint8_t* src_lds, unsigned ob, unsigned nbytes)
+{
+    // LDS byte ob + j -> dst[opos + j]; LDS word k <-> global dword (dst + opos - ob + 4k)
+    const unsigned lane = lane_id();
+    uint8_t* d = o.dst + o.opos;
+    const unsigned end = ob + nbytes;
+    const unsigned wfirst = (ob + 3) >> 2, wlast = end >> 2;   // whole words [wfirst, wlast)
+    uint32_t* gw = (uint32_t*)(d - ob);
+    const uint32_t* lw = (const uint32_t*)src_lds;
+    for (unsigned k = wfirst + lane; k < wlast; k += WAVE) gw[k] = lw[k];
+    // edges
+    if (lane < 4) {
+        const unsigned j = ob + lane;
+        if (j < end && j < wfirst * 4) d[j - ob] = src_lds[j];
+    } else if (lane < 8) {
+        const unsigned j = wlast * 4 + (lane - 4);
+        if (j >= ob && j < end && j >= wfirst * 4) d[j - ob] = src_lds[j];
+    }
+}
+
+template <int HIST>
+__device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base, unsigned len, const Params& P,
+                              MsgOut& o)
+{
+    using namespace lz;
+    const unsigned lane = lane_id();
+    const unsigned cend = base + CHUNK < len ? base + CHUNK : len;
+    const unsigned wb = base > (unsigned)HIST ? base - HIST : 0;
+    const unsigned wn = cend - wb, a0 = base - wb, clen = cend - base;
+    const bool stored_only = P.L.parser == P_STORED;
+
+    Win W;
+    W.w = S.win;
+    W.b = (const uint8_t*)S.win;
+    W.ws = 0;
+    HuffLds& H = S.a.h;
+    unsigned kind = 0;   // 0 stored, 1 fixed, 2 dynamic
+    LaneToks T;
+    T.kept = 0;
+    T.rem_kind = 0;
+    T.rem_len = T.rem_dist = T.rem_b0 = T.rem_b1 = 0;
+    T.lastdist = 0;
+    T.a = T.b = 0;
+    uint32_t hdr_bits = 0, blcodes = 0, lcodes = 0, dcodes = 0;
+
+    if (!stored_only) {
+        W.ws = load_window(S, msg + wb, wn);
+        const bool chains = P.strategy != 2 && P.strategy != 3;
+        if (chains) {
+            for (unsigned i = lane; i < HSIZE; i += WAVE) S.b.head[i] = 0xFFFFFFFFu;
+        }
+        wave_sync();
+        // ---- hash chains
+        if (chains) {
+            for (unsigned g = 0; g < wn; g += WAVE) {
+                const unsigned q = g + lane;
+                uint32_t pv = NONE;
+                if (q + MIN_MATCH <= wn) {
+                    const uint32_t h = hash3(W.dw(q), HB);
+                    const uint32_t pre = S.b.head[h];
+                    const uint32_t old = atomicExch(&S.b.head[h], q);
+                    const uint32_t c = old < q ? old : pre;
+                    atomicMax(&S.b.head[h], q);
+                    pv = c < NONE ? c : NONE;
+                }
+                if (q < wn) S.a.prev[q] = (uint16_t)pv;
+            }
+        }
+        wave_sync();
+        // ---- parse (head table dead from here; tok[] reuses it)
+        unsigned seg = (clen + WAVE - 1) / WAVE;
+        seg = seg < MIN_SEG ? MIN_SEG : seg;
+        const unsigned a = a0 + lane * seg;
+        const unsigned b = a + seg < wn ? a + seg : wn;
+        const bool active = a < wn;
+        uint64_t bm = 0;
+        unsigned own_end = 0, lastdist = 0;
+        if (active) {
+            const bool lazy = P.L.parser == P_SLOW;
+            unsigned p = a, l0 = 0, d0 = 0;
+            bool have0 = false;
+            while (p < b) {
+                if (have0 && !(lazy && l0 < P.L.lazy && p + 1 < wn)) {
+                    S.b.tok[p - a0] = (uint16_t)(0x8000u | (l0 - MIN_MATCH));
+                    if (p + 1 < b) S.b.tok[p + 1 - a0] = (uint16_t)(d0 - 1);
+                    else lastdist = d0;
+                    bm |= 1ull << (p - a);
+                    p += l0;
+                    have0 = false;
+                    continue;
+                }
+                const unsigned q = have0 ? p + 1 : p;
+                const unsigned thr = have0 ? l0 : (unsigned)(MIN_MATCH - 1);
+                unsigned d = 0;
+                const unsigned l = find_match(W, S.a.prev, q, wn, thr, P, d);
+                if (!have0) {
+                    if (l < (unsigned)MIN_MATCH) {
+                        S.b.tok[p - a0] = (uint16_t)W.byte(p);
+                        bm |= 1ull << (p - a);
+                        ++p;
+                    } else {
+                        l0 = l;
+                        d0 = d;
+                        have0 = true;
+                    }
+                } else if (l > l0) {
+                    S.b.tok[p - a0] = (uint16_t)W.byte(p);
+                    bm |= 1ull << (p - a);
+                    ++p;
+                    l0 = l;
+                    d0 = d;
+                } else {
+                    S.b.tok[p - a0] = (uint16_t)(0x8000u | (l0 - MIN_MATCH));
+                    if (p + 1 < b) S.b.tok[p + 1 - a0] = (uint16_t)(d0 - 1);
+                    else lastdist = d0;
+                    bm |= 1ull << (p - a);
+                    p += l0;
+                    have0 = false;
+                }
+            }
+            own_end = p;
+        }
+        wave_sync();
+        // ---- boundary repair
+        const unsigned E = wave_scan_max_excl(own_end, a0);
+        T.a = a;
+        T.b = b;
+        T.lastdist = lastdist;
+        if (active) {
+            const unsigned rel = E - a;
+            const uint64_t below = rel >= 64 ? bm : (bm & ((1ull << rel) - 1));
+            T.kept = rel >= 64 ? 0 : (bm & ~((1ull << rel) - 1));
+            if (below) {
+                const unsigned t = 63 - (unsigned)__builtin_clzll(below);
+                const unsigned pos = a + t;
+                const uint32_t e = S.b.tok[pos - a0];
+                const unsigned tl = (e & 0x8000u) ? (e & 0xFFu) + MIN_MATCH : 1;
+                if (pos + tl > E) {
+                    const unsigned r = pos + tl - E;
+                    if (tl > 1 && r >= (unsigned)MIN_MATCH) {
+                        T.rem_kind = 1;
+                        T.rem_len = r;
+                        T.rem_dist = pos + 1 < b ? (unsigned)S.b.tok[pos + 1 - a0] + 1 : lastdist;
+                    } else {
+                        T.rem_kind = 2;
+                        T.rem_len = r;
+                        T.rem_b0 = W.byte(E);
+                        T.rem_b1 = r > 1 ? W.byte(E + 1) : 0;
+                    }
+                }
+            }
+        }
+        // ---- histograms (prev[] is dead: all lanes left the parse)
+        for (unsigned i = lane; i < 288 + 32 + 20; i += WAVE) {
+            if (i < 288) H.lf[i] = 0;
+            else if (i < 320) H.df[i - 288] = 0;
+            else H.bf[i - 320] = 0;
+        }
+        wave_sync();
+        for_tokens(T, S.b.tok, a0, [&](bool is_match, unsigned v, unsigned dist) {
+            if (!is_match) { atomicAdd(&H.lf[v], 1u); return; }
+            unsigned s, nx, xv;
+            len_code(v, s, nx, xv);
+            atomicAdd(&H.lf[s], 1u);
+            dist_code(dist, s, nx, xv);
+            atomicAdd(&H.df[s], 1u);
+        });
+        wave_sync();
+        if (lane == 0) H.lf[EOB] = 1;
+        wave_sync();
+        build_trees(H);
+        canonical_codes(H, 0, N_LCODES);
+        canonical_codes(H, DIST_IDX, N_DCODES);
+        // ---- code-length code (lane 0) and block costs
+        {
+            unsigned ll = 0, dl = 0;
+            for (unsigned i = lane; i < N_LCODES; i += WAVE)
+                if (H.lens[i]) ll = i + 1;
+            for (unsigned i = lane; i < N_DCODES; i += WAVE)
+                if (H.lens[DIST_IDX + i]) dl = i + 1;
+            lcodes = wave_maxu(ll);
+            dcodes = wave_maxu(dl);
+            lcodes = lcodes < 257 ? 257 : lcodes;
+            dcodes = dcodes < 1 ? 1 : dcodes;
+        }
+        if (lane == 0) {
+            auto getl = [&](int i) { return (int)H.lens[i]; };
+            auto getd = [&](int i) { return (int)H.lens[DIST_IDX + i]; };
+            auto cnt = [&](int s, int, int) { H.bf[s]++; };
+            rle_lengths(getl, (int)lcodes, cnt);
+            rle_lengths(getd, (int)dcodes, cnt);
+            tiny_lengths(H.bf, N_BLCODES, MAX_BL_BITS, H.bll, H.keys, H.iw, H.parent, H.depth);
+            // canonical code-length codes
+            unsigned cntb[8] = {0}, next[8];
+            for (int s = 0; s < N_BLCODES; ++s) cntb[H.bll[s]]++;
+            cntb[0] = 0;
+            unsigned code = 0;
+            for (int b2 = 1; b2 <= MAX_BL_BITS; ++b2) { code = (code + cntb[b2 - 1]) << 1; next[b2] = code; }
+            for (int s = 0; s < N_BLCODES; ++s) H.blc[s] = H.bll[s] ? pack_code(next[H.bll[s]]++, H.bll[s]) : 0;
+            unsigned nbl = N_BLCODES;
+            while (nbl > 4 && H.bll[bl_order(nbl - 1)] == 0) --nbl;
+            uint32_t hb = 3 + 5 + 5 + 4 + 3 * nbl;
+            for (int s = 0; s < N_BLCODES; ++s)
+                hb += H.bf[s] * (H.bll[s] + (s == 16 ? 2u : s == 17 ? 3u : s == 18 ? 7u : 0u));
+            H.misc[0] = hb;
+            H.misc[1] = nbl;
+        }
+        uint32_t dyn = 0, fix = 0;
+        for (unsigned i = lane; i < N_LCODES; i += WAVE) {
+            const uint32_t f = H.lf[i];
+            const unsigned x = i > 256 ? len_extra_bits(i) : 0;
+            dyn += f * (H.lens[i] + x);
+            fix += f * (fixed_lit_len(i) + x);
+        }
+        if (lane < N_DCODES) {
+            const uint32_t f = H.df[lane];
+            dyn += f * (H.lens[DIST_IDX + lane] + dist_extra_bits(lane));
+            fix += f * (5 + dist_extra_bits(lane));
+        }
+        dyn = wave_sum(dyn);
+        fix = wave_sum(fix) + 3;
+        wave_sync();
+        hdr_bits = H.misc[0];
+        blcodes = H.misc[1];
+        dyn += hdr_bits;
+        uint32_t opt_b = (dyn + 7) >> 3;
+        const uint32_t fix_b = (fix + 7) >> 3;
+        if (P.strategy == 4) opt_b = fix_b + 1;
+        const uint32_t best = opt_b < fix_b ? opt_b : fix_b;
+        kind = (clen + 4 <= best) ? 0u : (fix_b <= opt_b ? 1u : 2u);
+    }
+
+    if (kind == 0) {
+        // ---- stored block: 000, pad, LEN, NLEN, bytes (tr_stored_block)
+        const unsigned hb = o.cbits + 3 > 8 ? 2u : 1u;
+        const unsigned total = hb + 4 + clen;
+        if (o.opos + total > o.cap) { o.overflow = true; return; }
+        uint8_t* d = o.dst + o.opos;
+        if (lane == 0) {
+            d[0] = (uint8_t)o.carry;
+            if (hb == 2) d[1] = 0;
+            d[hb + 0] = (uint8_t)(clen & 0xFF);
+            d[hb + 1] = (uint8_t)(clen >> 8);
+            d[hb + 2] = (uint8_t)(~clen & 0xFF);
+            d[hb + 3] = (uint8_t)((~clen >> 8) & 0xFF);
+        }
+        for (unsigned i = lane; i < clen; i += WAVE) d[hb + 4 + i] = msg[base + i];
+        o.opos += total;
+        o.carry = 0;
+        o.cbits = 0;
+        return;
+    }
+
+    // ---- Huffman block: codes table = fixed or dynamic
+    if (kind == 1) {
+        for (unsigned i = lane; i < N_LCODES; i += WAVE) {
+            unsigned l;
+            const unsigned c = fixed_code(i, l);
+            H.codes[i] = pack_code(c, l);
+        }
+        if (lane < N_DCODES) H.codes[DIST_IDX + lane] = pack_code(lane, 5);
+        hdr_bits = 3;
+    }
+    wave_sync();
+    // per-lane token bits
+    uint32_t nbits = 0;
+    for_tokens(T, S.b.tok, a0, [&](bool is_match, unsigned v, unsigned dist) {
+        if (!is_match) { nbits += H.codes[v] >> 16; return; }
+        unsigned s, nx, xv;
+        len_code(v, s, nx, xv);
+        nbits += (H.codes[s] >> 16) + nx;
+        dist_code(dist, s, nx, xv);
+        nbits += (H.codes[DIST_IDX + s] >> 16) + nx;
+    });
+    const uint32_t incl = wave_scan_incl(nbits);
+    const uint32_t tok_bits = __shfl(incl, WAVE - 1);
+    const uint32_t eob_len = H.codes[EOB] >> 16;
+    const unsigned ob = (unsigned)((uintptr_t)(o.dst + o.opos) & 3);
+    const uint32_t start_bits = ob * 8 + o.cbits;
+    const uint32_t total_bits = o.cbits + hdr_bits + tok_bits + eob_len;   // from the carry's first bit
+    const unsigned nbytes = (total_bits + 7) >> 3;
+    if (o.opos + nbytes > o.cap) { o.overflow = true; return; }
+    // zero the bit buffer (win is dead: literals live in tok[])
+    uint32_t* ow = S.win;
+    const unsigned nwords = (ob + nbytes + 3) >> 2;
+    for (unsigned i = lane; i < nwords + 1; i += WAVE) ow[i] = 0;
+    wave_sync();
+    if (lane == 0) {
+        BitOr bw;
+        bw.start(ow, ob * 8);
+        bw.put(o.carry, o.cbits);
+        if (kind == 1) {
+            bw.put(1u << 1, 3);
+        } else {
+            bw.put(2u << 1, 3);
+            bw.put(lcodes - 257, 5);
+            bw.put(dcodes - 1, 5);
+            bw.put(blcodes - 4, 4);
+            for (unsigned i = 0; i < blcodes; ++i) bw.put(H.bll[bl_order(i)], 3);
+            auto emit = [&](int s, int nx, int xv) {
+                const uint32_t c = H.blc[s];
+                bw.put(c & 0xFFFFu, c >> 16);
+                if (nx) bw.put((uint32_t)xv, (unsigned)nx);
+            };
+            auto getl = [&](int i) { return (int)H.lens[i]; };
+            auto getd = [&](int i) { return (int)H.lens[DIST_IDX + i]; };
+            rle_lengths(getl, (int)lcodes, emit);
+            rle_lengths(getd, (int)dcodes, emit);
+        }
+        // end of block after all tokens
+        BitOr be;
+        be.start(ow, start_bits + hdr_bits + tok_bits);
+        const uint32_t c = H.codes[EOB];
+        be.put(c & 0xFFFFu, c >> 16);
+        be.flush();
+        bw.flush();
+    }
+    {
+        BitOr bw;
+        bw.start(ow, start_bits + hdr_bits + (incl - nbits));
+        for_tokens(T, S.b.tok, a0, [&](bool is_match, unsigned v, unsigned dist) {
+            if (!is_match) {
+                const uint32_t c = H.codes[v];
+                bw.put(c & 0xFFFFu, c >> 16);
+                return;
+            }
+            unsigned s, nx, xv;
+            len_code(v, s, nx, xv);
+            uint32_t c = H.codes[s];
+            bw.put((c & 0xFFFFu) | (xv << (c >> 16)), (c >> 16) + nx);
+            dist_code(dist, s, nx, xv);
+            c = H.codes[DIST_IDX + s];
+            bw.put(c & 0xFFFFu, c >> 16);
+            if (nx) bw.put(xv, nx);
+        });
+        bw.flush();
+    }
+    wave_sync();
+    put_bytes_global(o, (const uint8_t*)ow, ob, nbytes);
+    const uint8_t* ob8 = (const uint8_t*)ow;
+    o.opos += total_bits >> 3;
+    o.cbits = total_bits & 7;
+    o.carry = o.cbits ? ob8[ob + (total_bits >> 3)] : 0u;
+    wave_sync();
+}
+
+template <int HIST>
+__global__ void __launch_bounds__(64)
+deflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint32_t* __restrict__ in_len,
+               uint32_t n, uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
+               const uint32_t* __restrict__ out_cap, uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
+               Params P)
+{
+    __shared__ DefLds<HIST> S;
+    const unsigned lane = lane_id();
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const uint32_t len = in_len[i];
+        if (HIST == 0 ? len > CHUNK : len <= CHUNK) continue;
+        MsgOut o;
+        o.dst = out + out_off[i];
+        o.cap = out_cap[i];
+        o.opos = 0;
+        o.carry = 0;
+        o.cbits = 0;
+        o.overflow = false;
+        const uint8_t* msg = in + in_off[i];
+        for (uint32_t base = 0; base < len && !o.overflow; base += CHUNK) deflate_chunk<HIST>(S, msg, base, len, P, o);
+        // Flush::sync's empty stored block header (000) + pad; 00 00 FF FF stripped
+        const unsigned tb = o.cbits + 3 > 8 ? 2u : 1u;
+        if (!o.overflow && o.opos + tb > o.cap) o.overflow = true;
+        if (lane == 0) {
+            if (!o.overflow) {
+                o.dst[o.opos] = (uint8_t)o.carry;
+                if (tb == 2) o.dst[o.opos + 1] = 0;
+            }
+            out_len[i] = o.overflow ? 0u : o.opos + tb;
+            status[i] = o.overflow ? ST_NEED_BUFFERS : ST_OK;
+        }
+        wave_sync();
+    }
+}
+
+}  // namespace dfl
+}  // namespace bpmd
+
+namespace {
+template <int HIST>
+int launch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n, uint8_t* out,
+           const uint64_t* out_off, const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
+           const bpmd::dfl::Params& P, hipStream_t stream)
+{
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const unsigned per_cu = (160u * 1024u) / (unsigned)sizeof(bpmd::dfl::DefLds<HIST>);
+    unsigned grid = (unsigned)cus * (per_cu ? per_cu : 1u);
+    if (grid > n) grid = n;
+    hipLaunchKernelGGL(bpmd::dfl::deflate_kernel<HIST>, dim3(grid), dim3(64), 0, stream, in, in_off, in_len, n, out,
+                       out_off, out_cap, out_len, status, P);
+    return (int)hipGetLastError();
+}
+}  // namespace
+
+extern "C" int bpmd_internal_deflate(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n,
+                                     uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                                     uint32_t* out_len, int32_t* status, int level, int window_bits, int strategy,
+                                     hipStream_t stream)
+{
+    bpmd::dfl::Params P;
+    P.L = lz::level_params(level);
+    P.strategy = strategy;
+    const unsigned wsize = 1u << window_bits;
+    P.max_dist = wsize - lz::LOOKAHEAD_MIN;
+    int e = launch<0>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, P, stream);
+    if (e) return e;
+    return launch<4096>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, P, stream);
+}

@@ -165,3 +165,35 @@ def inflate_batch(src: Batch, out_cap, window_bits: int = 15, raw: bool = False,
                                 _ptr(out_off), _ptr(cap), _ptr(out_len), _ptr(status), _stream_handle(stream)),
            "bpmd_inflate_batch")
     return Result(Batch(out, out_off, out_len), cap, status)
+
+
+def deflate_batch(src: Batch, level: int = 6, window_bits: int = 15, mem_level: int = 4, strategy: int = 0,
+                  stream=None, out_cap=None, out: torch.Tensor | None = None,
+                  out_off: torch.Tensor | None = None) -> Result:
+    """Deflate every message of `src` into a permessage-deflate payload
+    (tail stripped) on the current GPU, asynchronous on `stream`.
+
+    Slots default to deflate_upper_bound(len) bytes, which always suffices.
+    """
+    L = lib()
+    dev = src.data.device
+    n = src.n
+    if out_cap is None:
+        ln = src.len.to(torch.int64)
+        cap = (ln + (ln + 7) // 8 + (ln + 63) // 64 + 11).to(torch.int32)
+    elif isinstance(out_cap, int):
+        cap = torch.full((n,), out_cap, dtype=torch.int32, device=dev)
+    else:
+        cap = out_cap.to(device=dev, dtype=torch.int32)
+    if out_off is None:
+        out_off = slot_offsets(cap)
+    if out is None:
+        total = int(out_off[-1].item() + cap[-1].item()) if n else 0
+        out = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+    out_len = torch.empty(n, dtype=torch.int32, device=dev)
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+    cfg = _Cfg(level, window_bits, mem_level, strategy, 0)
+    _check(L.bpmd_deflate_batch(ctypes.byref(cfg), _ptr(src.data), _ptr(src.off), _ptr(src.len), n, _ptr(out),
+                                _ptr(out_off), _ptr(cap), _ptr(out_len), _ptr(status), _stream_handle(stream)),
+           "bpmd_deflate_batch")
+    return Result(Batch(out, out_off, out_len), cap, status)

@@ -96,6 +96,27 @@ int bpmd_inflate_batch(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t*
                        const uint64_t* d_out_off, const uint32_t* d_out_cap,
                        uint32_t* d_out_len, int32_t* d_status, void* stream);
 
+/* Batched deflate of independent messages into permessage-deflate payloads
+ * (replaces one zo.write(zs, Flush::none) ... zo.write(zs, Flush::block),
+ * zo.write(zs, Flush::sync), strip 00 00 FF FF, zo.reset() sequence per
+ * message under no_context_takeover: impl_base.hpp:85-166,
+ * websocket/impl/write.hpp:655-703).  cfg->level / window_bits / mem_level
+ * are validated as deflate_stream::reset (deflate_stream.ipp:227-265);
+ * strategy selects the parser as zlib::Strategy does.  The payload is a
+ * valid raw-DEFLATE stream whose blocks all have BFINAL = 0, ending with
+ * the header bits of an empty stored block padded to a byte, exactly the
+ * framing Beast produces; the block contents are this engine's own parse
+ * (byte-identical round trip, compressed size within the tolerance stated
+ * in DESIGN.md).
+ *   d_in + d_in_off[i], d_in_len[i]     message i
+ *   d_out + d_out_off[i], d_out_cap[i]  output slot i (bpmd_deflate_upper_bound(len) always suffices)
+ *   d_out_len[i]  payload bytes;  d_status[i]  0, or need_buffers if the
+ *                 slot was too small (d_out_len[i] = 0, slot contents undefined) */
+int bpmd_deflate_batch(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_off,
+                       const uint32_t* d_in_len, uint32_t n_msgs, uint8_t* d_out,
+                       const uint64_t* d_out_off, const uint32_t* d_out_cap,
+                       uint32_t* d_out_len, int32_t* d_status, void* stream);
+
 /* deflate_upper_bound (zlib/deflate_stream.hpp:402-410): size a d_out slot. */
 size_t bpmd_deflate_upper_bound(size_t n);
 

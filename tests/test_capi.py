@@ -42,3 +42,17 @@ def test_window_bits_validated_before_device_use():
     cfg = pmd._Cfg(6, 15, 4, 0, 0)
     r = L.bpmd_inflate_batch(ctypes.byref(cfg), None, None, None, 1, None, None, None, None, None, None)
     assert r == -1
+
+
+def test_deflate_parameters_validated_before_device_use():
+    # deflate_stream.ipp:235-253: bad level / windowBits / memLevel throw
+    # std::invalid_argument -> -1; level -1 and windowBits 8 are accepted
+    L = pmd.lib()
+    for lvl, wb, mem, st in ((10, 15, 4, 0), (-2, 15, 4, 0), (6, 7, 4, 0), (6, 16, 4, 0), (6, 15, 0, 0),
+                             (6, 15, 10, 0), (6, 15, 4, 5)):
+        cfg = pmd._Cfg(lvl, wb, mem, st, 0)
+        r = L.bpmd_deflate_batch(ctypes.byref(cfg), None, None, None, 1, None, None, None, None, None, None)
+        assert r == -1, (lvl, wb, mem, st)
+    for lvl, wb in ((-1, 15), (6, 8), (0, 9)):
+        cfg = pmd._Cfg(lvl, wb, 4, 0, 0)
+        assert L.bpmd_deflate_batch(ctypes.byref(cfg), None, None, None, 0, None, None, None, None, None, None) == 0
