@@ -1,17 +1,22 @@
 #!/usr/bin/env python3
 """Benchmark: device-resident permessage-deflate throughput on MI355X.
 
-Workload (BASELINE.json configs[1], "C2"): 64 Ki independent 4 KiB JSON-like
-WebSocket payloads per GPU, compressed with compLevel=6, memLevel=4,
-windowBits=15 and Beast's pmd framing (impl_base.hpp:85-154), resident in HBM.
-One step = one batched inflate launch over the whole batch.  The C3 round
-trip (GPU deflate + GPU inflate of the same shape) is reported alongside.
+Headline workload (BASELINE.json configs[1], "C2"): 64 Ki independent 4 KiB
+JSON-like WebSocket payloads per GPU, compressed with compLevel=6,
+memLevel=4, windowBits=15 and Beast's pmd framing (impl_base.hpp:85-154),
+resident in HBM.  One step = one batched inflate launch over the whole
+batch; `value` is that inflate rate.
+
+Also reported (same JSON line, key "deflate"): configs[2] ("C3"), the
+round trip of 64 Ki x 4 KiB JSON (seed 0x5EED0003) through the GPU deflater
+and back through the GPU inflater -- deflate GiB/s, round-trip GiB/s,
+compressed size vs Beast's deflate at the same level.
 
 Launch:  python bench.py [--gpus N --steps K --warmup W]
-N > 1 runs under torch.distributed.run: every rank inflates its own 64 Ki
-messages (messages are independent streams under no_context_takeover), so
-there is no collective on the data path; scaling is weak.  Timing is
-barrier + synchronize on both sides, max over ranks.
+N > 1 runs under torch.distributed.run: every rank works on its own 64 Ki
+messages (independent streams under no_context_takeover), so there is no
+collective on the data path; scaling is weak.  Timing is barrier +
+synchronize on both sides, max over ranks.
 """
 from __future__ import annotations
 
@@ -33,7 +38,8 @@ from beast_amd import pmd, synth  # noqa: E402
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 N_MSGS = 1 << 16
 MSG_BYTES = 4096
-SEED = 0x5EED0002
+SEED_C2 = 0x5EED0002
+SEED_C3 = 0x5EED0003
 
 
 def log(*a):
@@ -66,27 +72,55 @@ def pack(payloads, align=16):
     return buf, off, lens.astype(np.int32)
 
 
-def cpu_baseline(comp_buf, comp_off, comp_len, raw_lens, threads, budget_s=12.0):
+def _median3(fn):
+    times = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        fn()
+        times.append(time.perf_counter() - t0)
+    return sorted(times)[1]
+
+
+def cpu_inflate_baseline(comp_buf, comp_off, comp_len, raw_lens, threads, budget_s=8.0):
     """Oracle (C restatement of Beast's zlib, byte-identical to it) inflating
     the same payloads on the host cores; bounded sample."""
     from oracle import oracle as O
     n = len(comp_len)
-    # size the sample so one pass is ~1-2 s on the given threads
     t0 = time.perf_counter()
     k = min(n, 2048)
     O.inflate_batch(comp_buf, comp_off[:k], comp_len[:k], raw_lens[:k], threads=1)
     per_msg = (time.perf_counter() - t0) / k
     sample = int(min(n, max(4096, budget_s / 4 / max(per_msg, 1e-9) * threads)))
-    times = []
-    for _ in range(3):
-        t0 = time.perf_counter()
-        O.inflate_batch(comp_buf, comp_off[:sample], comp_len[:sample], raw_lens[:sample], threads=threads)
-        times.append(time.perf_counter() - t0)
-    t = sorted(times)[1]
+    t = _median3(lambda: O.inflate_batch(comp_buf, comp_off[:sample], comp_len[:sample], raw_lens[:sample],
+                                         threads=threads))
     gib = float(raw_lens[:sample].astype(np.int64).sum()) / (1 << 30)
     return {"value": round(gib / t, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": f"{sample} x {MSG_BYTES} B C2 payloads, oracle inflate (Beast-equivalent C), "
+            "sample": f"{sample} x {MSG_BYTES} B C2 payloads, oracle inflate (Beast-equivalent C restatement), "
                       f"{threads} threads, median of 3"}
+
+
+def cpu_deflate_baseline(raw, off, lens, threads, budget_s=8.0):
+    """Oracle deflate (byte-identical to Beast: L6, memLevel 4, w15, pmd
+    framing) on a bounded sample; also returns Beast's payload bytes for the
+    sample so the GPU size ratio is measured on the same messages."""
+    from oracle import oracle as O
+    n = len(lens)
+    k = min(n, 512)
+    t0 = time.perf_counter()
+    O.deflate_batch(raw, off[:k], lens[:k], level=6, mem_level=4, threads=1)
+    per_msg = (time.perf_counter() - t0) / k
+    sample = int(min(n, max(2048, budget_s / 4 / max(per_msg, 1e-9) * threads)))
+    res = {}
+
+    def run():
+        res["r"] = O.deflate_batch(raw, off[:sample], lens[:sample], level=6, mem_level=4, threads=threads)
+    t = _median3(run)
+    gib = float(lens[:sample].astype(np.int64).sum()) / (1 << 30)
+    beast_len = res["r"][2]
+    return ({"value": round(gib / t, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+             "sample": f"{sample} x {MSG_BYTES} B C3 messages, oracle deflate L6/mem4/w15 "
+                       f"(Beast-equivalent C restatement), {threads} threads, median of 3"},
+            sample, beast_len)
 
 
 def pmc_traffic(kernel):
@@ -109,6 +143,39 @@ def pmc_traffic(kernel):
     return None, None
 
 
+class Timer:
+    """K timed steps bracketed by barrier + synchronize; per-step HIP events
+    on the launch stream for the kernel-side average."""
+
+    def __init__(self, dist):
+        self.dist = dist
+
+    def run(self, step, steps, warmup):
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        if self.dist:
+            self.dist.barrier()
+        torch.cuda.synchronize()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        t0 = time.perf_counter()
+        for i in range(steps):
+            ev[i][0].record()
+            step()
+            ev[i][1].record()
+        torch.cuda.synchronize()
+        if self.dist:
+            self.dist.barrier()
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+        if self.dist:
+            t = torch.tensor([wall, kern_ms], dtype=torch.float64, device="cuda")
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+            wall, kern_ms = float(t[0]), float(t[1])
+        return wall / steps, kern_ms
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -116,6 +183,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--msgs", type=int, default=N_MSGS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-deflate", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -126,60 +194,38 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-
+    timer = Timer(dist)
+    dev = torch.device("cuda", local)
     n = args.msgs
-    t0 = time.perf_counter()
     lens = np.full(n, MSG_BYTES, dtype=np.uint32)
-    raw, raw_off, raw_len = synth.make_batch("json", lens, seed=SEED, first=rank * n)
+
+    # ------------------------------------------------------------ C2 inflate
+    t0 = time.perf_counter()
+    raw, raw_off, raw_len = synth.make_batch("json", lens, seed=SEED_C2, first=rank * n)
     payloads = pmd_compress_host(raw, raw_off, raw_len)
     comp_buf, comp_off, comp_len = pack(payloads)
-    log(f"[rank {rank}] inputs ready in {time.perf_counter() - t0:.1f}s, ratio "
+    log(f"[rank {rank}] C2 inputs ready in {time.perf_counter() - t0:.1f}s, ratio "
         f"{comp_len.sum() / raw_len.astype(np.int64).sum():.4f}")
-
-    dev = torch.device("cuda", local)
     src = pmd.Batch(torch.from_numpy(comp_buf).to(dev), torch.from_numpy(comp_off).to(dev),
                     torch.from_numpy(comp_len).to(dev))
     cap = torch.full((n,), MSG_BYTES, dtype=torch.int32, device=dev)
     out_off = pmd.slot_offsets(cap)
     out = torch.empty(n * MSG_BYTES + 64, dtype=torch.uint8, device=dev)
 
-    def step():
+    def inflate_step():
         return pmd.inflate_batch(src, cap, out=out, out_off=out_off)
 
-    # correctness gate (outside the timed region)
-    r = step()
+    r = inflate_step()
     torch.cuda.synchronize()
     ok = int((r.status != 0).sum()) == 0 and torch.equal(
         out[: n * MSG_BYTES].view(n, MSG_BYTES), torch.from_numpy(raw.reshape(n, MSG_BYTES)).to(dev))
     if not ok:
-        log(f"[rank {rank}] PARITY FAILURE")
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    t_start = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record()
-        step()
-        ev[i][1].record()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t_start
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    if dist:
-        t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall, kern_ms = float(t[0]), float(t[1])
+        log(f"[rank {rank}] C2 PARITY FAILURE")
+    step_s, kern_ms = timer.run(inflate_step, args.steps, args.warmup)
 
     uncomp = n * MSG_BYTES
     comp = int(comp_len.astype(np.int64).sum())
-    total_uncomp = uncomp * world
-    value = total_uncomp / (1 << 30) / (wall / args.steps)
+    value = uncomp * world / (1 << 30) / step_s
     alg_bytes = comp + uncomp + 16 * n
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic("inflate_kernel") if n == N_MSGS else (None, None)
@@ -190,7 +236,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(wall / args.steps * 1e3, 4),
+        "ms_per_step": round(step_s * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -206,9 +252,66 @@ def main():
                      "kernel": "inflate_kernel", "kernel_ms": round(kern_ms, 4),
                      "alg_bytes_per_launch": alg_bytes},
     }
+    del src, out, r
+
+    # ------------------------------------------------- C3 deflate round trip
+    if not args.no_deflate:
+        raw3, off3, len3 = synth.make_batch("json", lens, seed=SEED_C3, first=rank * n)
+        src3 = pmd.Batch(torch.from_numpy(raw3).to(dev), torch.from_numpy(off3.astype(np.int64)).to(dev),
+                         torch.from_numpy(len3.astype(np.int32)).to(dev))
+        ub = pmd.upper_bound(MSG_BYTES)
+        cap3 = torch.full((n,), ub, dtype=torch.int32, device=dev)
+        off3o = pmd.slot_offsets(cap3)
+        out3 = torch.empty(int(off3o[-1].item()) + ub + 64, dtype=torch.uint8, device=dev)
+
+        def deflate_step():
+            return pmd.deflate_batch(src3, level=6, mem_level=4, out_cap=cap3, out=out3, out_off=off3o)
+
+        d = deflate_step()
+        torch.cuda.synchronize()
+        comp_b = pmd.Batch(out3, off3o, d.out.len.clone())
+        cap_in = torch.full((n,), MSG_BYTES, dtype=torch.int32, device=dev)
+        rt_off = pmd.slot_offsets(cap_in)
+        rt_out = torch.empty(n * MSG_BYTES + 64, dtype=torch.uint8, device=dev)
+
+        def reinflate_step():
+            return pmd.inflate_batch(comp_b, cap_in, out=rt_out, out_off=rt_off)
+
+        rr = reinflate_step()
+        torch.cuda.synchronize()
+        ok3 = (int((d.status != 0).sum()) == 0 and int((rr.status != 0).sum()) == 0
+               and torch.equal(rt_out[: n * MSG_BYTES].view(n, MSG_BYTES), src3.data[: n * MSG_BYTES].view(n, MSG_BYTES)))
+        if not ok3:
+            log(f"[rank {rank}] C3 ROUND-TRIP FAILURE")
+        gpu_len = d.out.len.cpu().numpy().astype(np.int64)
+        d_step, d_kern = timer.run(deflate_step, args.steps, args.warmup)
+        i_step, i_kern = timer.run(reinflate_step, args.steps, args.warmup)
+        comp3 = int(gpu_len.sum())
+        dval = uncomp * world / (1 << 30) / d_step
+        dalg = uncomp + comp3 + 16 * n
+        result["deflate"] = {
+            "workload": "C3 round trip: 64Ki x 4KiB JSON/GPU (seed 0x5EED0003), GPU deflate L6 then GPU inflate",
+            "deflate_value": round(dval, 3), "deflate_ms_per_step": round(d_step * 1e3, 4),
+            "roundtrip_value": round(uncomp * world / (1 << 30) / (d_step + i_step), 3),
+            "inflate_of_gpu_payloads_value": round(uncomp * world / (1 << 30) / i_step, 3),
+            "unit": "GiB/s", "roundtrip_ok": bool(ok3),
+            "ratio": round(comp3 / uncomp, 4),
+            "roofline": {"bound": "hbm", "achieved": round(dalg / (d_kern * 1e-3) / 1e9, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(dalg / (d_kern * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                         "kernel": "deflate_kernel", "kernel_ms": round(d_kern, 4), "alg_bytes_per_launch": dalg},
+        }
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            threads = min(16, os.cpu_count() or 1)
+            cb, sample, beast_len = cpu_deflate_baseline(raw3, off3, len3, threads)
+            result["deflate"]["cpu_baseline"] = cb
+            result["deflate"]["size_vs_beast"] = round(float(gpu_len[:sample].sum()) / float(beast_len.sum()), 4)
+            result["deflate"]["size_sample"] = f"first {sample} messages, Σ GPU bytes / Σ Beast bytes at L6/mem4"
+        del src3, out3, rt_out, d, rr
+
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
-        result["cpu_baseline"] = cpu_baseline(comp_buf, comp_off, comp_len, raw_len.astype(np.uint32), threads)
+        result["cpu_baseline"] = cpu_inflate_baseline(comp_buf, comp_off, comp_len, raw_len.astype(np.uint32),
+                                                      threads)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:
