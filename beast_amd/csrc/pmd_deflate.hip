@@ -9,7 +9,7 @@
 // empty stored block (000) and byte padding, with the 00 00 FF FF tail
 // stripped.  The block contents are this kernel's own parse (the contract is
 // a byte-identical round trip and a compressed-size tolerance, not
-// bit-identity with zlib); scripts/deflate_model.cpp is the host model of
+// bit-identity with zlib); tests/model/deflate_model.cpp is the host model of
 // exactly this algorithm.
 //
 // Per 4 KiB chunk of a message (small messages: one chunk, no history; large
@@ -52,7 +52,14 @@ struct HuffLds {
     uint32_t lf[288];
     uint32_t df[32];
     uint32_t bf[20];
-    uint32_t keys[512];
+    union {
+        uint32_t keys[512];          // sort buffer (tree build)
+        struct {
+            uint16_t sym[320];       // run-length coded code lengths: sym | extra << 5
+            uint64_t start[6];       // run-start bitmap over the code-length sequence
+            uint32_t tkey[24];       // code-length-code tree keys
+        } r;
+    };
     uint16_t iw[320];            // internal node weights: lit [0, 288), dist [288, 320)
     uint16_t parent[NODES];
     uint8_t depth[NODES];
@@ -82,7 +89,27 @@ struct Params {
     lz::Level L;
     int strategy;        // bpmd_strategy
     unsigned max_dist;   // w_size - MIN_LOOKAHEAD
+    unsigned chain;      // chain limit (level table, capped for single-chunk messages)
 };
+
+// Diagnostic build only (-DBPMD_PROF): per-phase wave cycles and counts.
+__device__ unsigned long long g_dprof[24];
+#ifdef BPMD_PROF
+struct Prof {
+    unsigned long long c[24];
+    unsigned long long t;
+    __device__ Prof() : t(__builtin_amdgcn_s_memtime()) { for (int i = 0; i < 24; ++i) c[i] = 0; }
+    __device__ void lap(int i) { const unsigned long long t2 = __builtin_amdgcn_s_memtime(); c[i] += t2 - t; t = t2; }
+    __device__ void cnt(int i, unsigned long long n) { c[i] += n; }
+    __device__ void flush() { if (lane_id() == 0) for (int i = 0; i < 24; ++i) atomicAdd(&g_dprof[i], c[i]); }
+};
+#else
+struct Prof {
+    __device__ void lap(int) {}
+    __device__ void cnt(int, unsigned long long) {}
+    __device__ void flush() {}
+};
+#endif
 
 // ------------------------------------------------------------------ window
 
@@ -97,7 +124,21 @@ struct Win {
         const uint32_t lo = w[j >> 2], hi = w[(j >> 2) + 1];
         return __builtin_amdgcn_alignbit(hi, lo, (j & 3) * 8);
     }
+    // 8 bytes starting at window byte i (little-endian)
+    __device__ __forceinline__ uint64_t qw(unsigned i) const
+    {
+        const unsigned j = ws + i, k = j >> 2, sh = (j & 3) * 8;
+        const uint32_t w0 = w[k], w1 = w[k + 1], w2 = w[k + 2];
+        return ((uint64_t)__builtin_amdgcn_alignbit(w2, w1, sh) << 32) | __builtin_amdgcn_alignbit(w1, w0, sh);
+    }
 };
+
+// number of equal leading bytes of two 8-byte groups (8 = all)
+__device__ __forceinline__ unsigned eq_bytes(uint64_t a, uint64_t b)
+{
+    const uint64_t x = a ^ b;
+    return x ? (unsigned)__builtin_ctzll(x) >> 3 : 8u;
+}
 
 template <int HIST>
 __device__ __forceinline__ unsigned load_window(DefLds<HIST>& S, const uint8_t* src, unsigned nbytes)
@@ -109,67 +150,6 @@ __device__ __forceinline__ unsigned load_window(DefLds<HIST>& S, const uint8_t* 
     uint4* l = (uint4*)S.win;
     for (unsigned u = lane_id(); u < units; u += WAVE) l[u] = g[u];
     return s;
-}
-
-// -------------------------------------------------------------- matching
-
-__device__ __forceinline__ unsigned match_len(const Win& W, unsigned c, unsigned p, unsigned maxl)
-{
-    unsigned l = 0;
-    for (;;) {
-        const uint32_t x = W.dw(c + l) ^ W.dw(p + l);
-        if (x) { l += (unsigned)__builtin_ctz(x) >> 3; break; }
-        l += 4;
-        if (l >= maxl) break;
-    }
-    return l < maxl ? l : maxl;
-}
-
-// longest_match restated per lane (deflate_stream.ipp:1747-1844), window
-// coordinates; returns the best length (> thr) or thr.
-__device__ __forceinline__ unsigned find_match(const Win& W, const uint16_t* prev, unsigned q, unsigned end,
-                                               unsigned thr, const Params& P, unsigned& dist)
-{
-    using namespace lz;
-    if (P.strategy == 2 || q + MIN_MATCH > end) return thr;
-    const unsigned maxl = end - q < (unsigned)MAX_MATCH ? end - q : (unsigned)MAX_MATCH;
-    if (P.strategy == 3) {   // rle: distance one only (f_rle, deflate_stream.ipp:2190-2270)
-        if (q == 0) return thr;
-        const uint32_t v = W.byte(q - 1) * 0x01010101u;
-        unsigned l = 0;
-        for (;;) {
-            const uint32_t x = W.dw(q + l) ^ v;
-            if (x) { l += (unsigned)__builtin_ctz(x) >> 3; break; }
-            l += 4;
-            if (l >= maxl) break;
-        }
-        l = l < maxl ? l : maxl;
-        if (l > thr && l >= (unsigned)MIN_MATCH) { dist = 1; return l; }
-        return thr;
-    }
-    unsigned chain = P.L.chain;
-    if (thr >= P.L.good) chain >>= 2;
-    const unsigned nice = P.L.nice < maxl ? P.L.nice : maxl;
-    unsigned best = thr, bd = 0;
-    const uint32_t b0 = W.byte(q);
-    uint32_t pb = best < maxl ? W.byte(q + best) : 0;
-    uint32_t c = prev[q];
-    while (c != NONE && q - c <= P.max_dist && chain-- > 0) {
-        if (best < maxl && W.byte(c + best) == pb && W.byte(c) == b0) {
-            const unsigned l = match_len(W, c, q, maxl);
-            if (l > best) {
-                best = l;
-                bd = q - c;
-                if (l >= nice) break;
-                pb = best < maxl ? W.byte(q + best) : 0;
-            }
-        }
-        c = prev[c];
-    }
-    if (best > thr && best <= 5 && (P.strategy == 1 || (best == (unsigned)MIN_MATCH && bd > (unsigned)TOO_FAR)))
-        return thr;
-    if (best > thr) dist = bd;
-    return best;
 }
 
 // ---------------------------------------------------------------- bit sink
@@ -332,7 +312,7 @@ __device__ __forceinline__ void tiny_lengths(const uint32_t* freq, unsigned n, u
 
 // Lit/len and distance code lengths + canonical codes for the current
 // histograms (H.lf with EOB counted, H.df).  Whole wave.
-__device__ void build_trees(HuffLds& H)
+__device__ void build_trees(HuffLds& H, Prof& pf)
 {
     const unsigned lane = lane_id();
     // --- keys, with the reference's "at least two codes" dummies
@@ -365,7 +345,7 @@ __device__ void build_trees(HuffLds& H)
 #pragma unroll
             for (unsigned t = 0; t < 4; ++t) {
                 const unsigned i = lane + t * WAVE;
-                const unsigned lo = ((i / j) * 2 * j) + (i % j), hi = lo + j;
+                const unsigned lo = ((i & ~(j - 1)) << 1) | (i & (j - 1)), hi = lo + j;
                 const uint32_t x = H.keys[lo], y = H.keys[hi];
                 const bool up = (lo & k) == 0;
                 if ((x > y) == up) { H.keys[lo] = y; H.keys[hi] = x; }
@@ -373,6 +353,7 @@ __device__ void build_trees(HuffLds& H)
             wave_sync();
         }
     }
+    pf.lap(4);
     const unsigned ml = used_l, md = used_d;
     // --- merges (lane 0: lit, lane 1: dist)
     if (lane < 2) {
@@ -380,6 +361,7 @@ __device__ void build_trees(HuffLds& H)
         else merge_tree(H, ml, md, 288, 576);
     }
     wave_sync();
+    pf.lap(5);
     // --- depths by pointer jumping over both trees
     const unsigned root_l = 2 * ml - 2, root_d = 576 + 2 * md - 2;
     {
@@ -426,6 +408,7 @@ __device__ void build_trees(HuffLds& H)
             if (!ballot(any)) break;
         }
     }
+    pf.lap(6);
     // --- length limit (15) and per-length counts
     for (unsigned i = lane; i < 32; i += WAVE) H.blcount[i >> 4][i & 15] = 0;
     wave_sync();
@@ -563,7 +546,7 @@ __device__ __forceinline__ void put_bytes_global(MsgOut& o, const uint8_t* src_l
 
 template <int HIST>
 __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base, unsigned len, const Params& P,
-                              MsgOut& o)
+                              MsgOut& o, Prof& pf)
 {
     using namespace lz;
     const unsigned lane = lane_id();
@@ -584,7 +567,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
     T.rem_len = T.rem_dist = T.rem_b0 = T.rem_b1 = 0;
     T.lastdist = 0;
     T.a = T.b = 0;
-    uint32_t hdr_bits = 0, blcodes = 0, lcodes = 0, dcodes = 0;
+    uint32_t hdr_bits = 0, blcodes = 0, lcodes = 0, dcodes = 0, nrle = 0;
 
     if (!stored_only) {
         W.ws = load_window(S, msg + wb, wn);
@@ -593,6 +576,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
             for (unsigned i = lane; i < HSIZE; i += WAVE) S.b.head[i] = 0xFFFFFFFFu;
         }
         wave_sync();
+        pf.lap(0);
         // ---- hash chains
         if (chains) {
             for (unsigned g = 0; g < wn; g += WAVE) {
@@ -610,6 +594,8 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
             }
         }
         wave_sync();
+        pf.lap(1);
+        [[maybe_unused]] unsigned steps = 0, finds = 0, iters = 0;
         // ---- parse (head table dead from here; tok[] reuses it)
         unsigned seg = (clen + WAVE - 1) / WAVE;
         seg = seg < MIN_SEG ? MIN_SEG : seg;
@@ -619,51 +605,122 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
         uint64_t bm = 0;
         unsigned own_end = 0, lastdist = 0;
         if (active) {
+            // The reference's parse loop (f_fast / f_slow) and longest_match
+            // chain walk, flattened into one state machine so that every
+            // iteration does one unit of work per lane (a parse decision, one
+            // chain candidate, or 8 more bytes of a match) -- nested
+            // divergent loops would multiply lane imbalance.
             const bool lazy = P.L.parser == P_SLOW;
+            const bool no_match = P.strategy == 2, rle = P.strategy == 3;
+            const unsigned chain_max = P.chain;
             unsigned p = a, l0 = 0, d0 = 0;
             bool have0 = false;
+            // Each iteration is one predicated step for every lane:
+            //   start  the find at q was just set up: take the chain head
+            //   chain  test candidate c (quick reject on the byte at `best`,
+            //          first 8 bytes compared)
+            //   match  compare 8 more bytes of the match with c
+            // with every load issued up front from mode-independent
+            // addresses.  Only the parse decision after a finished find
+            // branches.
+            bool st = true, mt = false;      // start / match state (chain otherwise)
+            unsigned q = p, thr = MIN_MATCH - 1, c = 0, chain_left = 0, best = thr, bd = 0, nice = 0, maxl = 0,
+                     l = 0;
             while (p < b) {
-                if (have0 && !(lazy && l0 < P.L.lazy && p + 1 < wn)) {
-                    S.b.tok[p - a0] = (uint16_t)(0x8000u | (l0 - MIN_MATCH));
-                    if (p + 1 < b) S.b.tok[p + 1 - a0] = (uint16_t)(d0 - 1);
-                    else lastdist = d0;
-                    bm |= 1ull << (p - a);
-                    p += l0;
-                    have0 = false;
-                    continue;
+                ++iters;
+                const unsigned cc = c < wn ? c : 0;
+                const uint32_t pn = S.a.prev[st ? q : cc];
+                const uint32_t cb = W.byte(cc + best), qb = W.byte(q + best);
+                const uint64_t cv = W.qw(cc + l), qv = W.qw(q + l);
+                const unsigned k = eq_bytes(cv, qv);
+                const bool ch = !st && !mt;
+                const bool term = ch && (c == NONE || q - c > P.max_dist || chain_left == 0);
+                const bool test = ch && !term;
+                const bool quick = test && best < maxl && cb == qb && k > 0;
+                const bool go_match = quick && k == 8 && maxl > 8;
+                const bool ext = mt && k == 8 && l + 8 < maxl;
+                const bool have_len = (quick && !go_match) || (mt && !ext);
+                const unsigned len = l + k < maxl ? l + k : maxl;
+                const bool improve = have_len && len > best;
+                if (improve) {
+                    best = len;
+                    bd = q - c;
                 }
-                const unsigned q = have0 ? p + 1 : p;
-                const unsigned thr = have0 ? l0 : (unsigned)(MIN_MATCH - 1);
-                unsigned d = 0;
-                const unsigned l = find_match(W, S.a.prev, q, wn, thr, P, d);
-                if (!have0) {
-                    if (l < (unsigned)MIN_MATCH) {
+                const bool start_done = st && (no_match || q + MIN_MATCH > wn);
+                const bool found = term || start_done || (improve && len >= nice);
+                steps += test;
+                chain_left -= test;
+                const bool advance = !found && ((test && !go_match) || (mt && !ext));
+                l = go_match ? 8u : ext ? l + 8 : 0u;
+                if (st) {
+                    maxl = wn - q < (unsigned)MAX_MATCH ? wn - q : (unsigned)MAX_MATCH;
+                    c = rle ? (q > 0 ? q - 1 : NONE) : pn;
+                    chain_left = rle ? 1u : (thr >= P.L.good ? chain_max >> 2 : chain_max);
+                    nice = rle ? maxl : (P.L.nice < maxl ? P.L.nice : maxl);
+                } else if (advance) {
+                    c = pn;
+                }
+                mt = go_match || ext;
+                st = false;
+                if (found) {
+                    unsigned lr = best;
+                    if (best > thr && best <= 5 &&
+                        (P.strategy == 1 || (best == (unsigned)MIN_MATCH && bd > (unsigned)TOO_FAR)))
+                        lr = thr;
+                    // f_slow / f_fast decision
+                    bool lit = false, emit = false;
+                    unsigned el = 0, ed = 0;
+                    if (!have0) {
+                        if (lr < (unsigned)MIN_MATCH) lit = true;
+                        else { l0 = lr; d0 = bd; have0 = true; }
+                    } else if (lr > l0) {
+                        lit = true;
+                        l0 = lr;
+                        d0 = bd;
+                    } else {
+                        emit = true;
+                        el = l0;
+                        ed = d0;
+                        have0 = false;
+                    }
+                    if (lit) {
                         S.b.tok[p - a0] = (uint16_t)W.byte(p);
                         bm |= 1ull << (p - a);
                         ++p;
-                    } else {
-                        l0 = l;
-                        d0 = d;
-                        have0 = true;
                     }
-                } else if (l > l0) {
-                    S.b.tok[p - a0] = (uint16_t)W.byte(p);
-                    bm |= 1ull << (p - a);
-                    ++p;
-                    l0 = l;
-                    d0 = d;
-                } else {
-                    S.b.tok[p - a0] = (uint16_t)(0x8000u | (l0 - MIN_MATCH));
-                    if (p + 1 < b) S.b.tok[p + 1 - a0] = (uint16_t)(d0 - 1);
-                    else lastdist = d0;
-                    bm |= 1ull << (p - a);
-                    p += l0;
-                    have0 = false;
+                    if (!emit && have0 && p < b && !(lazy && l0 < P.L.lazy && p + 1 < wn)) {
+                        emit = true;
+                        el = l0;
+                        ed = d0;
+                        have0 = false;
+                    }
+                    if (emit) {
+                        S.b.tok[p - a0] = (uint16_t)(0x8000u | (el - MIN_MATCH));
+                        if (p + 1 < b) S.b.tok[p + 1 - a0] = (uint16_t)(ed - 1);
+                        else lastdist = ed;
+                        bm |= 1ull << (p - a);
+                        p += el;
+                    }
+                    q = have0 ? p + 1 : p;
+                    thr = have0 ? l0 : (unsigned)(MIN_MATCH - 1);
+                    best = thr;
+                    bd = 0;
+                    st = true;
+                    mt = false;
+                    ++finds;
                 }
             }
             own_end = p;
         }
         wave_sync();
+        pf.lap(2);
+#ifdef BPMD_PROF
+        pf.cnt(19, wave_sum(steps));
+        pf.cnt(20, wave_maxu(steps));
+        pf.cnt(21, wave_sum(finds));
+        pf.cnt(18, 1);
+        pf.cnt(22, wave_maxu(iters));
+#endif
         // ---- boundary repair
         const unsigned E = wave_scan_max_excl(own_end, a0);
         T.a = a;
@@ -711,9 +768,12 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
         wave_sync();
         if (lane == 0) H.lf[EOB] = 1;
         wave_sync();
-        build_trees(H);
+        pf.lap(3);
+        build_trees(H, pf);
+        pf.lap(7);
         canonical_codes(H, 0, N_LCODES);
         canonical_codes(H, DIST_IDX, N_DCODES);
+        pf.lap(8);
         // ---- code-length code (lane 0) and block costs
         {
             unsigned ll = 0, dl = 0;
@@ -726,13 +786,49 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
             lcodes = lcodes < 257 ? 257 : lcodes;
             dcodes = dcodes < 1 ? 1 : dcodes;
         }
+        {
+            // Code-length sequence (lit lens, then dist lens; runs never
+            // cross the two) coded run by run (lz::rle_run == the reference's
+            // scan_tree/send_tree): run starts by ballot, run lengths from
+            // the start bitmap, symbol counts, prefix sum, symbols to
+            // H.r.sym and their histogram to H.bf.
+            const unsigned N = lcodes + dcodes;
+            auto val = [&](unsigned i) -> unsigned { return i < lcodes ? H.lens[i] : H.lens[DIST_IDX + i - lcodes]; };
+            for (unsigned c0 = 0; c0 < 320; c0 += WAVE) {
+                const unsigned i = c0 + lane;
+                const bool st = i == N || (i < N && (i == 0 || i == lcodes || val(i) != val(i - 1)));
+                const uint64_t m = ballot(st);
+                if (lane == 0) H.r.start[c0 >> 6] = m;
+            }
+            wave_sync();
+            uint32_t run_carry = 0;
+            for (unsigned c0 = 0; c0 < 320; c0 += WAVE) {
+                const unsigned i = c0 + lane;
+                const bool st = i < N && ((H.r.start[i >> 6] >> (i & 63)) & 1);
+                unsigned v = 0, r = 0, ns = 0;
+                if (st) {
+                    v = val(i);
+                    unsigned w = i >> 6;
+                    uint64_t m = H.r.start[w] & ~((2ull << (i & 63)) - 1);
+                    while (!m) m = H.r.start[++w];
+                    r = (w << 6) + (unsigned)__builtin_ctzll(m) - i;
+                    ns = rle_run_count(v, r);
+                }
+                const uint32_t incl = wave_scan_incl(ns);
+                uint32_t pos = run_carry + incl - ns;
+                if (st) {
+                    rle_run(v, r, [&](int s, int, int x) {
+                        H.r.sym[pos++] = (uint16_t)(s | (x << 5));
+                        atomicAdd(&H.bf[s], 1u);
+                    });
+                }
+                run_carry += __shfl(incl, WAVE - 1);
+            }
+            nrle = run_carry;
+            wave_sync();
+        }
         if (lane == 0) {
-            auto getl = [&](int i) { return (int)H.lens[i]; };
-            auto getd = [&](int i) { return (int)H.lens[DIST_IDX + i]; };
-            auto cnt = [&](int s, int, int) { H.bf[s]++; };
-            rle_lengths(getl, (int)lcodes, cnt);
-            rle_lengths(getd, (int)dcodes, cnt);
-            tiny_lengths(H.bf, N_BLCODES, MAX_BL_BITS, H.bll, H.keys, H.iw, H.parent, H.depth);
+            tiny_lengths(H.bf, N_BLCODES, MAX_BL_BITS, H.bll, H.r.tkey, H.iw, H.parent, H.depth);
             // canonical code-length codes
             unsigned cntb[8] = {0}, next[8];
             for (int s = 0; s < N_BLCODES; ++s) cntb[H.bll[s]]++;
@@ -748,6 +844,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
             H.misc[0] = hb;
             H.misc[1] = nbl;
         }
+        pf.lap(9);
         uint32_t dyn = 0, fix = 0;
         for (unsigned i = lane; i < N_LCODES; i += WAVE) {
             const uint32_t f = H.lf[i];
@@ -771,6 +868,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
         if (P.strategy == 4) opt_b = fix_b + 1;
         const uint32_t best = opt_b < fix_b ? opt_b : fix_b;
         kind = (clen + 4 <= best) ? 0u : (fix_b <= opt_b ? 1u : 2u);
+        pf.lap(10);
     }
 
     if (kind == 0) {
@@ -791,6 +889,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
         o.opos += total;
         o.carry = 0;
         o.cbits = 0;
+        pf.lap(11);
         return;
     }
 
@@ -825,6 +924,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
     if (o.opos + nbytes > o.cap) { o.overflow = true; return; }
     // zero the bit buffer (win is dead: literals live in tok[])
     uint32_t* ow = S.win;
+    pf.lap(12);
     const unsigned nwords = (ob + nbytes + 3) >> 2;
     for (unsigned i = lane; i < nwords + 1; i += WAVE) ow[i] = 0;
     wave_sync();
@@ -840,15 +940,6 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
             bw.put(dcodes - 1, 5);
             bw.put(blcodes - 4, 4);
             for (unsigned i = 0; i < blcodes; ++i) bw.put(H.bll[bl_order(i)], 3);
-            auto emit = [&](int s, int nx, int xv) {
-                const uint32_t c = H.blc[s];
-                bw.put(c & 0xFFFFu, c >> 16);
-                if (nx) bw.put((uint32_t)xv, (unsigned)nx);
-            };
-            auto getl = [&](int i) { return (int)H.lens[i]; };
-            auto getd = [&](int i) { return (int)H.lens[DIST_IDX + i]; };
-            rle_lengths(getl, (int)lcodes, emit);
-            rle_lengths(getd, (int)dcodes, emit);
         }
         // end of block after all tokens
         BitOr be;
@@ -858,6 +949,28 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
         be.flush();
         bw.flush();
     }
+    if (kind == 2) {
+        // run-length coded code lengths, one symbol per lane per step
+        uint32_t at = start_bits + 3 + 5 + 5 + 4 + 3 * blcodes;
+        for (unsigned c0 = 0; c0 < nrle; c0 += WAVE) {
+            const unsigned k = c0 + lane;
+            uint32_t nb = 0, v = 0;
+            if (k < nrle) {
+                const uint32_t e = H.r.sym[k], s = e & 31u, x = e >> 5;
+                const uint32_t code = H.blc[s], cl = code >> 16;
+                v = (code & 0xFFFFu) | (x << cl);
+                nb = cl + (s == 16 ? 2u : s == 17 ? 3u : s == 18 ? 7u : 0u);
+            }
+            const uint32_t incl2 = wave_scan_incl(nb);
+            if (nb) {
+                const uint32_t bp = at + incl2 - nb, sh = bp & 31;
+                atomicOr(&ow[bp >> 5], v << sh);
+                if (sh + nb > 32) atomicOr(&ow[(bp >> 5) + 1], v >> (32 - sh));
+            }
+            at += __shfl(incl2, WAVE - 1);
+        }
+    }
+    pf.lap(13);
     {
         BitOr bw;
         bw.start(ow, start_bits + hdr_bits + (incl - nbits));
@@ -879,12 +992,14 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
         bw.flush();
     }
     wave_sync();
+    pf.lap(14);
     put_bytes_global(o, (const uint8_t*)ow, ob, nbytes);
     const uint8_t* ob8 = (const uint8_t*)ow;
     o.opos += total_bits >> 3;
     o.cbits = total_bits & 7;
     o.carry = o.cbits ? ob8[ob + (total_bits >> 3)] : 0u;
     wave_sync();
+    pf.lap(15);
 }
 
 template <int HIST>
@@ -896,6 +1011,7 @@ deflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
 {
     __shared__ DefLds<HIST> S;
     const unsigned lane = lane_id();
+    Prof pf;
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
         const uint32_t len = in_len[i];
         if (HIST == 0 ? len > CHUNK : len <= CHUNK) continue;
@@ -907,7 +1023,7 @@ deflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
         o.cbits = 0;
         o.overflow = false;
         const uint8_t* msg = in + in_off[i];
-        for (uint32_t base = 0; base < len && !o.overflow; base += CHUNK) deflate_chunk<HIST>(S, msg, base, len, P, o);
+        for (uint32_t base = 0; base < len && !o.overflow; base += CHUNK) deflate_chunk<HIST>(S, msg, base, len, P, o, pf);
         // Flush::sync's empty stored block header (000) + pad; 00 00 FF FF stripped
         const unsigned tb = o.cbits + 3 > 8 ? 2u : 1u;
         if (!o.overflow && o.opos + tb > o.cap) o.overflow = true;
@@ -921,6 +1037,7 @@ deflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
         }
         wave_sync();
     }
+    pf.flush();
 }
 
 }  // namespace dfl
@@ -953,7 +1070,20 @@ extern "C" int bpmd_internal_deflate(const uint8_t* in, const uint64_t* in_off, 
     P.strategy = strategy;
     const unsigned wsize = 1u << window_bits;
     P.max_dist = wsize - lz::LOOKAHEAD_MIN;
+    P.chain = lz::gpu_chain(level, true);
     int e = launch<0>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, P, stream);
     if (e) return e;
+    P.chain = lz::gpu_chain(level, false);
     return launch<4096>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, P, stream);
+}
+
+extern "C" int bpmd_diag_deflate_counters(unsigned long long* out, int reset)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(bpmd::dfl::g_dprof), sizeof(unsigned long long) * 24) != hipSuccess)
+        return -1;
+    if (reset) {
+        unsigned long long z[24] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(bpmd::dfl::g_dprof), z, sizeof z) != hipSuccess) return -1;
+    }
+    return 0;
 }

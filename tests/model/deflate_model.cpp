@@ -140,6 +140,8 @@ static std::vector<uint8_t> encode(const uint8_t* msg, unsigned n, const Params&
     BitW bw;
     bw.out = &out;
     Level L = level_params(P.level);
+    Params Q = P;   // the kernel's chain limit for this message
+    if (!Q.chain_cap) Q.chain_cap = (int)gpu_chain(P.level, n <= (unsigned)P.chunk);
     unsigned wsize = 1u << (P.wbits < 9 ? 9 : P.wbits);
     unsigned max_dist = wsize - LOOKAHEAD_MIN;
     std::vector<int32_t> prev;
@@ -166,7 +168,7 @@ static std::vector<uint8_t> encode(const uint8_t* msg, unsigned n, const Params&
             for (unsigned s = a0; s < wn; s += seg) {
                 unsigned b = s + seg < wn ? s + seg : wn;
                 std::vector<Tok> lt;
-                parse_segment(w, prev.data(), s, b, wn, P, L, max_dist, lt);
+                parse_segment(w, prev.data(), s, b, wn, Q, L, max_dist, lt);
                 // boundary repair against the previous segments' end E
                 for (const Tok& t : lt) {
                     if (t.pos + t.len <= E) continue;
@@ -278,4 +280,28 @@ extern "C" int64_t dmodel_batch(const uint8_t* data, const uint64_t* off, const 
         pos += e.size();
     }
     return (int64_t)pos;
+}
+
+// Self-check hook: code-length run-length coding of `lens[0..n)` by the
+// serial state machine and by the per-run closed form the kernel uses;
+// writes both symbol streams (sym | extra << 8) and returns 1 if equal.
+extern "C" int dmodel_rle_check(const uint8_t* lens, int n, uint32_t* serial, uint32_t* runs, int* ns, int* nr)
+{
+    int a = 0, b = 0;
+    auto get = [&](int i) { return (int)lens[i]; };
+    rle_lengths(get, n, [&](int s, int, int x) { serial[a++] = (uint32_t)s | ((uint32_t)x << 8); });
+    unsigned cnt = 0;
+    for (int i = 0; i < n;) {
+        int j = i + 1;
+        while (j < n && lens[j] == lens[i]) ++j;
+        cnt += rle_run_count(lens[i], (unsigned)(j - i));
+        rle_run(lens[i], (unsigned)(j - i), [&](int s, int, int x) { runs[b++] = (uint32_t)s | ((uint32_t)x << 8); });
+        i = j;
+    }
+    *ns = a;
+    *nr = b;
+    if (a != b || (unsigned)b != cnt) return 0;
+    for (int i = 0; i < a; ++i)
+        if (serial[i] != runs[i]) return 0;
+    return 1;
 }

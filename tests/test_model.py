@@ -44,3 +44,31 @@ def test_model_size_within_tolerance_of_beast():
     ours = sum(len(p) for p in pl)
     beast = sum(len(O.pmd_deflate(m, 6, 15, 4)) for m in msgs)
     assert ours <= 1.10 * beast, ours / beast
+
+
+def test_runwise_code_length_coding_equals_serial_state_machine():
+    """The kernel codes code-length runs independently (lz::rle_run); it must
+    reproduce the reference's scan_tree/send_tree state machine
+    (deflate_stream.ipp:978-1110) symbol for symbol."""
+    import ctypes
+    import random
+    L = M.lib()
+    rng = random.Random(3)
+    out1 = (ctypes.c_uint32 * 400)()
+    out2 = (ctypes.c_uint32 * 400)()
+    na, nb = ctypes.c_int(), ctypes.c_int()
+    for trial in range(3000):
+        n = rng.randrange(1, 320)
+        mode = trial % 3
+        if mode == 0:
+            lens = [rng.choice([0, 0, 0, 5, 6, 7, 8]) for _ in range(n)]
+        elif mode == 1:
+            lens = []
+            while len(lens) < n:
+                lens += [rng.randrange(0, 16)] * rng.randrange(1, 160)
+            lens = lens[:n]
+        else:
+            lens = [rng.randrange(0, 16) for _ in range(n)]
+        buf = (ctypes.c_uint8 * n)(*lens)
+        ok = L.dmodel_rle_check(buf, n, out1, out2, ctypes.byref(na), ctypes.byref(nb))
+        assert ok == 1, (lens, na.value, nb.value)
