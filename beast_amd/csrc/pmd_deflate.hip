@@ -90,6 +90,7 @@ struct Params {
     int strategy;        // bpmd_strategy
     unsigned max_dist;   // w_size - MIN_LOOKAHEAD
     unsigned chain;      // chain limit (level table, capped for single-chunk messages)
+    uint32_t* out_bits;  // optional: payload length in bits before the sync-marker tail
 };
 
 // Diagnostic build only (-DBPMD_PROF): per-phase wave cycles and counts.
@@ -1033,6 +1034,7 @@ deflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
                 if (tb == 2) o.dst[o.opos + 1] = 0;
             }
             out_len[i] = o.overflow ? 0u : o.opos + tb;
+            if (P.out_bits) P.out_bits[i] = o.overflow ? 0u : o.opos * 8 + o.cbits;
             status[i] = o.overflow ? ST_NEED_BUFFERS : ST_OK;
         }
         wave_sync();
@@ -1060,21 +1062,31 @@ int launch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, ui
 }
 }  // namespace
 
-extern "C" int bpmd_internal_deflate(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n,
-                                     uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
-                                     uint32_t* out_len, int32_t* status, int level, int window_bits, int strategy,
-                                     hipStream_t stream)
+extern "C" int bpmd_internal_deflate_bits(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                          uint32_t n, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                                          uint32_t* out_len, int32_t* status, uint32_t* out_bits, int level,
+                                          int window_bits, int strategy, hipStream_t stream)
 {
     bpmd::dfl::Params P;
     P.L = lz::level_params(level);
     P.strategy = strategy;
     const unsigned wsize = 1u << window_bits;
     P.max_dist = wsize - lz::LOOKAHEAD_MIN;
+    P.out_bits = out_bits;
     P.chain = lz::gpu_chain(level, true);
     int e = launch<0>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, P, stream);
     if (e) return e;
     P.chain = lz::gpu_chain(level, false);
     return launch<4096>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, P, stream);
+}
+
+extern "C" int bpmd_internal_deflate(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n,
+                                     uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                                     uint32_t* out_len, int32_t* status, int level, int window_bits, int strategy,
+                                     hipStream_t stream)
+{
+    return bpmd_internal_deflate_bits(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, nullptr, level,
+                                      window_bits, strategy, stream);
 }
 
 extern "C" int bpmd_diag_deflate_counters(unsigned long long* out, int reset)

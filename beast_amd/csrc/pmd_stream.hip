@@ -1,0 +1,352 @@
+// pmd_stream.hip -- per-stream entry points behind the C++ compatibility
+// facade (include/beast_amd/zlib.hpp): zlib::deflate_stream /
+// zlib::inflate_stream write() semantics at message granularity, executed
+// by the batch kernels on the GPU (a batch of one).  Host code only.
+//
+// deflate: input is buffered until a flush; each flush compresses the
+//   buffered bytes on the GPU (blocks with BFINAL = 0, exact bit length
+//   returned by the kernel) and appends the flush's own bits the way the
+//   reference's doWrite does (deflate_stream.ipp:357-499): Flush::block
+//   leaves the last partial byte pending, partial adds tr_align's empty
+//   static block, sync/full add the empty stored block 000 + pad +
+//   00 00 FF FF, finish adds a final empty block and reports end_of_stream.
+//   Pending output, duplicate-flush need_buffers, stream_error and
+//   invalid_argument follow doWrite.
+// inflate: every write() appends its input to the message buffer and
+//   decodes the whole buffer again on the GPU with the output capacity
+//   (already delivered + avail_out), handing out the bytes past those
+//   already delivered -- the same bytes the reference's incremental
+//   decoder produces; all input is reported consumed.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/beast_pmd.h"
+
+extern "C" int bpmd_internal_inflate(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                        uint32_t n, uint8_t* out, const uint64_t* out_off,
+                                        const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
+                                        uint32_t raw, hipStream_t stream);
+extern "C" int bpmd_internal_deflate_bits(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                          uint32_t n, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                                          uint32_t* out_len, int32_t* status, uint32_t* out_bits, int level,
+                                          int window_bits, int strategy, hipStream_t stream);
+
+struct bpmd_stream {
+    bool is_deflate = true;
+    // deflate parameters
+    int level = 6, wbits = 15, mem_level = 9, strategy = 0;
+    // inflate parameters
+    int inf_wbits = 15;
+    // buffered input (deflate: message bytes; inflate: compressed bytes)
+    std::vector<uint8_t> in;
+    // deflate: output not yet handed out, plus < 8 pending bits
+    std::vector<uint8_t> pend;
+    size_t pend_pos = 0;
+    uint32_t bits = 0;
+    unsigned nbits = 0;
+    int last_flush = -1;        // boost::none
+    bool finished = false;      // finish_state
+    // inflate: bytes already handed out
+    size_t delivered = 0;
+    // device scratch
+    hipStream_t hs = nullptr;
+    uint8_t* dmem = nullptr;
+    size_t dcap = 0;
+};
+
+namespace {
+
+// device block layout: [meta 64 B][input][output]
+struct DevLayout {
+    size_t in_off, out_off, total;
+};
+
+int ensure_device(bpmd_stream* s, size_t need)
+{
+    if (!s->hs && hipStreamCreateWithFlags(&s->hs, hipStreamNonBlocking) != hipSuccess) return BPMD_R_HIP_ERROR;
+    if (need <= s->dcap) return BPMD_R_OK;
+    if (s->dmem) (void)hipFree(s->dmem);
+    s->dmem = nullptr;
+    s->dcap = 0;
+    size_t cap = std::max<size_t>(need, 1 << 16);
+    if (hipMalloc(&s->dmem, cap) != hipSuccess) return BPMD_R_HIP_ERROR;
+    s->dcap = cap;
+    return BPMD_R_OK;
+}
+
+struct Meta {
+    uint64_t in_off, out_off;
+    uint32_t in_len, out_cap, out_len, bits;
+    int32_t status;
+    uint32_t pad[6];
+};
+static_assert(sizeof(Meta) == 64, "meta block");
+
+// one message through a batch kernel; returns 0 or a negative bpmd_result
+int run_one(bpmd_stream* s, bool deflate, const uint8_t* in, size_t n, size_t out_cap, std::vector<uint8_t>& out,
+            int32_t& status, uint32_t& bits)
+{
+    if (n > 0xFFFFFFFFu || out_cap > 0xFFFFFFFFu) return BPMD_R_INVALID_ARGUMENT;
+    int r = bpmd_init();
+    if (r) return r;
+    const size_t in_at = 64, out_at = (in_at + n + 15) & ~size_t(15);
+    if ((r = ensure_device(s, out_at + out_cap + 16)) != 0) return r;
+    Meta m{};
+    m.in_off = 0;
+    m.out_off = 0;
+    m.in_len = (uint32_t)n;
+    m.out_cap = (uint32_t)out_cap;
+    uint8_t* d = s->dmem;
+    if (hipMemcpyAsync(d, &m, sizeof m, hipMemcpyHostToDevice, s->hs) != hipSuccess) return BPMD_R_HIP_ERROR;
+    if (n && hipMemcpyAsync(d + in_at, in, n, hipMemcpyHostToDevice, s->hs) != hipSuccess) return BPMD_R_HIP_ERROR;
+    Meta* dm = (Meta*)d;
+    int e;
+    if (deflate)
+        e = bpmd_internal_deflate_bits(d + in_at, &dm->in_off, &dm->in_len, 1, d + out_at, &dm->out_off, &dm->out_cap,
+                                       &dm->out_len, &dm->status, &dm->bits, s->level, s->wbits, s->strategy, s->hs);
+    else
+        e = bpmd_internal_inflate(d + in_at, &dm->in_off, &dm->in_len, 1, d + out_at, &dm->out_off, &dm->out_cap,
+                                  &dm->out_len, &dm->status, 1u, s->hs);
+    if (e) return BPMD_R_HIP_ERROR;
+    if (hipMemcpyAsync(&m, d, sizeof m, hipMemcpyDeviceToHost, s->hs) != hipSuccess) return BPMD_R_HIP_ERROR;
+    if (hipStreamSynchronize(s->hs) != hipSuccess) return BPMD_R_HIP_ERROR;
+    out.resize(m.out_len);
+    if (m.out_len && hipMemcpy(out.data(), d + out_at, m.out_len, hipMemcpyDeviceToHost) != hipSuccess)
+        return BPMD_R_HIP_ERROR;
+    status = m.status;
+    bits = m.bits;
+    return BPMD_R_OK;
+}
+
+// ------------------------------------------------------------ deflate bits
+
+void put_bits(bpmd_stream* s, uint32_t v, unsigned n)
+{
+    s->bits |= v << s->nbits;
+    s->nbits += n;
+    while (s->nbits >= 8) {
+        s->pend.push_back((uint8_t)s->bits);
+        s->bits >>= 8;
+        s->nbits -= 8;
+    }
+}
+
+// append `nb` bits of the little-endian bit string p
+void put_bitstring(bpmd_stream* s, const uint8_t* p, uint64_t nb)
+{
+    uint64_t i = 0;
+    if (s->nbits == 0) {
+        const size_t whole = (size_t)(nb >> 3);
+        s->pend.insert(s->pend.end(), p, p + whole);
+        i = (uint64_t)whole * 8;
+    }
+    for (; i + 8 <= nb; i += 8) put_bits(s, p[i >> 3], 8);
+    if (i < nb) put_bits(s, p[i >> 3] & ((1u << (nb - i)) - 1), (unsigned)(nb - i));
+}
+
+void align_bits(bpmd_stream* s)
+{
+    if (s->nbits) put_bits(s, 0, 8 - s->nbits);
+}
+
+void drain(bpmd_stream* s, bpmd_zparams* zs)
+{
+    const size_t avail = s->pend.size() - s->pend_pos;
+    const size_t k = std::min(avail, zs->avail_out);
+    if (k) {
+        std::memcpy(zs->next_out, s->pend.data() + s->pend_pos, k);
+        zs->next_out = (uint8_t*)zs->next_out + k;
+        zs->avail_out -= k;
+        zs->total_out += k;
+        s->pend_pos += k;
+    }
+    if (s->pend_pos == s->pend.size()) {
+        s->pend.clear();
+        s->pend_pos = 0;
+    }
+}
+
+bool has_pending(const bpmd_stream* s) { return s->pend_pos < s->pend.size(); }
+
+void reset_deflate(bpmd_stream* s)
+{
+    s->in.clear();
+    s->pend.clear();
+    s->pend_pos = 0;
+    s->bits = 0;
+    s->nbits = 0;
+    s->last_flush = -1;
+    s->finished = false;
+}
+
+}  // namespace
+
+extern "C" int bpmd_deflate_stream_create(int level, int window_bits, int mem_level, int strategy,
+                                          bpmd_stream** out)
+{
+    if (!out) return BPMD_R_INVALID_ARGUMENT;
+    *out = nullptr;
+    // deflate_stream.ipp:235-253
+    if (level == -1) level = 6;
+    if (window_bits == 8) window_bits = 9;
+    if (level < 0 || level > 9 || window_bits < 8 || window_bits > 15 || mem_level < 1 || mem_level > 9 ||
+        strategy < BPMD_STRATEGY_NORMAL || strategy > BPMD_STRATEGY_FIXED)
+        return BPMD_R_INVALID_ARGUMENT;
+    bpmd_stream* s = new (std::nothrow) bpmd_stream();
+    if (!s) return BPMD_R_INVALID_ARGUMENT;
+    s->is_deflate = true;
+    s->level = level;
+    s->wbits = window_bits;
+    s->mem_level = mem_level;
+    s->strategy = strategy;
+    *out = s;
+    return BPMD_R_OK;
+}
+
+extern "C" int bpmd_deflate_stream_reset(bpmd_stream* s)
+{
+    if (!s || !s->is_deflate) return BPMD_R_INVALID_ARGUMENT;
+    reset_deflate(s);
+    return BPMD_R_OK;
+}
+
+extern "C" int bpmd_deflate_stream_write(bpmd_stream* s, bpmd_zparams* zs, int flush)
+{
+    if (!s || !s->is_deflate || !zs || flush < BPMD_FLUSH_NONE || flush > BPMD_FLUSH_TREES)
+        return BPMD_R_INVALID_ARGUMENT;
+    if (!zs->next_in && zs->avail_in) return BPMD_R_INVALID_ARGUMENT;   // throws invalid_argument
+    if (!zs->next_out || (s->finished && flush != BPMD_FLUSH_FINISH)) return BPMD_STREAM_ERROR;
+    if (zs->avail_out == 0) return BPMD_NEED_BUFFERS;
+    const int old = s->last_flush;
+    s->last_flush = flush;
+    if (has_pending(s)) {
+        drain(s, zs);
+        if (zs->avail_out == 0) {
+            s->last_flush = -1;
+            return BPMD_OK;
+        }
+    } else if (zs->avail_in == 0 && old >= 0 && flush <= old && flush != BPMD_FLUSH_FINISH) {
+        return BPMD_NEED_BUFFERS;
+    }
+    if (s->finished && zs->avail_in) return BPMD_NEED_BUFFERS;
+    if (zs->avail_in) {
+        const uint8_t* p = (const uint8_t*)zs->next_in;
+        s->in.insert(s->in.end(), p, p + zs->avail_in);
+        zs->next_in = p + zs->avail_in;
+        zs->total_in += zs->avail_in;
+        zs->avail_in = 0;
+    }
+    if (flush != BPMD_FLUSH_NONE && !s->finished) {
+        if (!s->in.empty()) {
+            std::vector<uint8_t> out;
+            int32_t st = 0;
+            uint32_t nb = 0;
+            const size_t cap = bpmd_deflate_upper_bound(s->in.size()) + 16;
+            int r = run_one(s, true, s->in.data(), s->in.size(), cap, out, st, nb);
+            if (r) return r;
+            if (st != BPMD_OK) return BPMD_STREAM_ERROR;
+            put_bitstring(s, out.data(), nb);
+            s->in.clear();
+        }
+        switch (flush) {
+        case BPMD_FLUSH_PARTIAL:     // tr_align: empty static block
+            put_bits(s, 1u << 1, 3);
+            put_bits(s, 0, 7);
+            break;
+        case BPMD_FLUSH_SYNC:
+        case BPMD_FLUSH_FULL:        // tr_stored_block(nullptr, 0): 000, pad, 00 00 FF FF
+            put_bits(s, 0, 3);
+            align_bits(s);
+            put_bits(s, 0x0000, 16);
+            put_bits(s, 0xFFFF, 16);
+            break;
+        case BPMD_FLUSH_FINISH:      // last block: empty fixed block with BFINAL = 1
+            put_bits(s, 1u | (1u << 1), 3);
+            put_bits(s, 0, 7);
+            align_bits(s);
+            s->finished = true;
+            break;
+        default:                     // block / trees: the block is complete, bits stay pending
+            break;
+        }
+        drain(s, zs);
+        if (zs->avail_out == 0) s->last_flush = -1;
+    }
+    if (flush == BPMD_FLUSH_FINISH) return has_pending(s) ? BPMD_OK : BPMD_END_OF_STREAM;
+    return BPMD_OK;
+}
+
+extern "C" int bpmd_inflate_stream_create(int window_bits, bpmd_stream** out)
+{
+    if (!out) return BPMD_R_INVALID_ARGUMENT;
+    *out = nullptr;
+    if (window_bits < 8 || window_bits > 15) return BPMD_R_DOMAIN_ERROR;   // inflate_stream.ipp:57-61
+    bpmd_stream* s = new (std::nothrow) bpmd_stream();
+    if (!s) return BPMD_R_INVALID_ARGUMENT;
+    s->is_deflate = false;
+    s->inf_wbits = window_bits;
+    *out = s;
+    return BPMD_R_OK;
+}
+
+extern "C" int bpmd_inflate_stream_reset(bpmd_stream* s, int window_bits)
+{
+    if (!s || s->is_deflate) return BPMD_R_INVALID_ARGUMENT;
+    if (window_bits < 8 || window_bits > 15) return BPMD_R_DOMAIN_ERROR;
+    s->inf_wbits = window_bits;
+    s->in.clear();
+    s->delivered = 0;
+    return BPMD_R_OK;
+}
+
+extern "C" int bpmd_inflate_stream_clear(bpmd_stream* s)
+{
+    // inflate_stream::clear -> doClear is empty in the reference
+    // (inflate_stream.ipp:49-53): state and window persist
+    return (!s || s->is_deflate) ? BPMD_R_INVALID_ARGUMENT : BPMD_R_OK;
+}
+
+extern "C" int bpmd_inflate_stream_write(bpmd_stream* s, bpmd_zparams* zs, int flush)
+{
+    if (!s || s->is_deflate || !zs || flush < BPMD_FLUSH_NONE || flush > BPMD_FLUSH_TREES)
+        return BPMD_R_INVALID_ARGUMENT;
+    if ((!zs->next_in && zs->avail_in) || (!zs->next_out && zs->avail_out)) return BPMD_STREAM_ERROR;
+    const size_t n_in = zs->avail_in;
+    if (n_in) {
+        const uint8_t* p = (const uint8_t*)zs->next_in;
+        s->in.insert(s->in.end(), p, p + n_in);
+    }
+    std::vector<uint8_t> out;
+    int32_t st = BPMD_OK;
+    uint32_t nb = 0;
+    int r = run_one(s, false, s->in.data(), s->in.size(), s->delivered + zs->avail_out, out, st, nb);
+    if (r) {
+        if (n_in) s->in.resize(s->in.size() - n_in);
+        return r;
+    }
+    const size_t fresh = out.size() > s->delivered ? out.size() - s->delivered : 0;
+    if (fresh) std::memcpy(zs->next_out, out.data() + s->delivered, fresh);
+    s->delivered += fresh;
+    zs->next_in = (const uint8_t*)zs->next_in + n_in;
+    zs->avail_in = 0;
+    zs->total_in += n_in;
+    zs->next_out = (uint8_t*)zs->next_out + fresh;
+    zs->avail_out -= fresh;
+    zs->total_out += fresh;
+    zs->data_type = 2;   // unknown
+    if (st >= BPMD_END_OF_STREAM) return st;                // end_of_stream or a data error
+    if ((n_in == 0 && fresh == 0) || flush == BPMD_FLUSH_FINISH) return BPMD_NEED_BUFFERS;   // done()
+    return BPMD_OK;
+}
+
+extern "C" void bpmd_stream_destroy(bpmd_stream* s)
+{
+    if (!s) return;
+    if (s->dmem) (void)hipFree(s->dmem);
+    if (s->hs) (void)hipStreamDestroy(s->hs);
+    delete s;
+}

@@ -120,6 +120,52 @@ int bpmd_deflate_batch(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t*
 /* deflate_upper_bound (zlib/deflate_stream.hpp:402-410): size a d_out slot. */
 size_t bpmd_deflate_upper_bound(size_t n);
 
+/* ---------------------------------------------------------------------
+ * Per-stream API behind the C++ compatibility facade
+ * (include/beast_amd/zlib.hpp).  Host buffers; each call runs the batch
+ * kernels on the current device for one message and synchronises.
+ * Throughput comes from the batch API above; these calls exist so code
+ * written against zlib::deflate_stream / zlib::inflate_stream (the calls
+ * impl_base<true> makes, impl_base.hpp:85-190) runs unchanged.
+ * ------------------------------------------------------------------- */
+
+/* z_params (zlib/zlib.hpp:78-144) */
+typedef struct bpmd_zparams {
+    const void* next_in;
+    size_t avail_in;
+    size_t total_in;
+    void* next_out;
+    size_t avail_out;
+    size_t total_out;
+    int data_type;
+} bpmd_zparams;
+
+/* zlib::Flush (zlib/zlib.hpp:159-183); the order matters */
+enum bpmd_flush {
+    BPMD_FLUSH_NONE = 0, BPMD_FLUSH_BLOCK, BPMD_FLUSH_PARTIAL, BPMD_FLUSH_SYNC, BPMD_FLUSH_FULL,
+    BPMD_FLUSH_FINISH, BPMD_FLUSH_TREES
+};
+
+typedef struct bpmd_stream bpmd_stream;
+
+/* deflate_stream::reset(level, windowBits, memLevel, strategy)
+ * (deflate_stream.ipp:227-265); BPMD_R_INVALID_ARGUMENT where it throws */
+int bpmd_deflate_stream_create(int level, int window_bits, int mem_level, int strategy, bpmd_stream** out);
+/* deflate_stream::reset() (deflate_stream.hpp:123-127) */
+int bpmd_deflate_stream_reset(bpmd_stream* s);
+/* deflate_stream::write(zs, flush, ec) (deflate_stream.ipp:357-499): returns
+ * the zlib::error value (0 = none) or BPMD_R_INVALID_ARGUMENT where it throws */
+int bpmd_deflate_stream_write(bpmd_stream* s, bpmd_zparams* zs, int flush);
+/* inflate_stream::reset(windowBits) (inflate_stream.ipp:55-72);
+ * BPMD_R_DOMAIN_ERROR where it throws */
+int bpmd_inflate_stream_create(int window_bits, bpmd_stream** out);
+int bpmd_inflate_stream_reset(bpmd_stream* s, int window_bits);
+/* inflate_stream::clear() -- a no-op in the reference (inflate_stream.ipp:49-53) */
+int bpmd_inflate_stream_clear(bpmd_stream* s);
+/* inflate_stream::write(zs, flush, ec) (inflate_stream.ipp:74-535) */
+int bpmd_inflate_stream_write(bpmd_stream* s, bpmd_zparams* zs, int flush);
+void bpmd_stream_destroy(bpmd_stream* s);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,103 @@
+"""End-to-end (PCIe-inclusive) rate: the path starts and ends in host memory
+(Boost.Asio socket buffers), so this times pinned host -> device copy,
+kernel, device -> host copy for the C2 inflate batch and the C3 deflate
+batch, pipelined in chunks over two HIP streams (copy of chunk i+1 overlaps
+the kernel of chunk i).  Reported in DESIGN.md; never the bench `value`.
+
+    python scripts/e2e.py [--chunks 8] [--reps 5]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+from beast_amd import pmd, synth  # noqa: E402
+
+
+def chunk_views(buf, off, lens, nchunks):
+    n = len(lens)
+    per = (n + nchunks - 1) // nchunks
+    out = []
+    for c in range(nchunks):
+        s, e = c * per, min(n, (c + 1) * per)
+        base, end = int(off[s]), int(off[e - 1] + lens[e - 1])
+        out.append((torch.from_numpy(np.ascontiguousarray(buf[base:end])).pin_memory(),
+                    torch.from_numpy((off[s:e] - base).astype(np.int64)).pin_memory(),
+                    torch.from_numpy(lens[s:e].astype(np.int32)).pin_memory(), e - s))
+    return out
+
+
+def run_pipeline(chunks, kernel, out_bytes_of, reps):
+    dev = torch.device("cuda", 0)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    maxin = max(c[0].numel() for c in chunks)
+    maxn = max(c[3] for c in chunks)
+    slots = [dict(d=torch.empty(maxin + 64, dtype=torch.uint8, device=dev),
+                  o=torch.empty(maxn, dtype=torch.int64, device=dev),
+                  l=torch.empty(maxn, dtype=torch.int32, device=dev)) for _ in streams]
+    outs_h = [torch.empty(out_bytes_of(c[3]), dtype=torch.uint8).pin_memory() for c in chunks]
+    lens_h = [torch.empty(c[3], dtype=torch.int32).pin_memory() for c in chunks]
+    times = []
+    for _ in range(reps + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i, (hd, ho, hl, n) in enumerate(chunks):
+            s = streams[i % 2]
+            sl = slots[i % 2]
+            with torch.cuda.stream(s):
+                sl["d"][: hd.numel()].copy_(hd, non_blocking=True)
+                sl["o"][:n].copy_(ho, non_blocking=True)
+                sl["l"][:n].copy_(hl, non_blocking=True)
+                src = pmd.Batch(sl["d"], sl["o"][:n], sl["l"][:n])
+                res = kernel(src, s)
+                outs_h[i].copy_(res.out.data[: outs_h[i].numel()], non_blocking=True)
+                lens_h[i].copy_(res.out.len, non_blocking=True)
+                sl["keep"] = res
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    return sorted(times[1:])[len(times[1:]) // 2], outs_h, lens_h
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--chunks", type=int, default=8)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--msgs", type=int, default=bench.N_MSGS)
+    a = ap.parse_args()
+    n, mb = a.msgs, bench.MSG_BYTES
+    lens = np.full(n, mb, dtype=np.uint32)
+    res = {}
+
+    # C2 inflate: compressed payloads in, 4 KiB messages out
+    raw, roff, rlen = synth.make_batch("json", lens, seed=bench.SEED_C2)
+    comp, coff, clen = bench.pack(bench.pmd_compress_host(raw, roff, rlen))
+    chunks = chunk_views(comp, coff, clen, a.chunks)
+    t, outs, _ = run_pipeline(chunks, lambda src, s: pmd.inflate_batch(src, mb, stream=s), lambda k: k * mb, a.reps)
+    got = np.concatenate([o.numpy() for o in outs])
+    res["inflate_e2e_GiBps"] = round(n * mb / (1 << 30) / t, 3)
+    res["inflate_e2e_ok"] = bool(np.array_equal(got, raw[: n * mb]))
+    res["inflate_h2d_bytes"] = int(comp.nbytes)
+
+    # C3 deflate: messages in, payloads out (slots of upper_bound bytes)
+    raw3, off3, len3 = synth.make_batch("json", lens, seed=bench.SEED_C3)
+    ub = pmd.upper_bound(mb)
+    slot = (ub + 15) // 16 * 16
+    chunks3 = chunk_views(raw3, off3, len3, a.chunks)
+    t3, outs3, lens3 = run_pipeline(chunks3, lambda src, s: pmd.deflate_batch(src, level=6, stream=s),
+                                    lambda k: k * slot, a.reps)
+    res["deflate_e2e_GiBps"] = round(n * mb / (1 << 30) / t3, 3)
+    res["deflate_d2h_bytes"] = int(sum(int(x.numpy().sum()) for x in lens3))
+    res["chunks"] = a.chunks
+    res["streams"] = 2
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,177 @@
+"""GPU: per-stream API (the C++ facade's backend) driven exactly the way
+websocket::stream drives Beast's codec -- impl_base<true>::deflate
+(impl_base.hpp:85-154) with a 4 KiB write buffer, and the sync read path
+(read.hpp:1284-1356) with 1536-byte rd_buf slices and inflate_with_eb
+(impl_base.hpp:179-190).  Checked against the batch kernels and the
+oracle (Beast's inflate restated)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from beast_amd import synth
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+NONE, BLOCK, PARTIAL, SYNC, FULL, FINISH, TREES = range(7)
+
+
+class ZParams(ctypes.Structure):
+    _fields_ = [("next_in", ctypes.c_void_p), ("avail_in", ctypes.c_size_t), ("total_in", ctypes.c_size_t),
+                ("next_out", ctypes.c_void_p), ("avail_out", ctypes.c_size_t), ("total_out", ctypes.c_size_t),
+                ("data_type", ctypes.c_int)]
+
+
+def _lib():
+    from beast_amd import pmd
+    L = pmd.lib()
+    vp = ctypes.c_void_p
+    L.bpmd_deflate_stream_create.argtypes = [ctypes.c_int] * 4 + [ctypes.POINTER(vp)]
+    L.bpmd_inflate_stream_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+    L.bpmd_deflate_stream_write.argtypes = [vp, ctypes.POINTER(ZParams), ctypes.c_int]
+    L.bpmd_inflate_stream_write.argtypes = [vp, ctypes.POINTER(ZParams), ctypes.c_int]
+    L.bpmd_deflate_stream_reset.argtypes = [vp]
+    L.bpmd_inflate_stream_reset.argtypes = [vp, ctypes.c_int]
+    L.bpmd_stream_destroy.argtypes = [vp]
+    return L
+
+
+def _mk(L, deflate=True, level=6):
+    h = ctypes.c_void_p()
+    r = L.bpmd_deflate_stream_create(level, 15, 4, 0, ctypes.byref(h)) if deflate else \
+        L.bpmd_inflate_stream_create(15, ctypes.byref(h))
+    assert r == 0
+    return h
+
+
+def ws_deflate_message(L, zo, msg: bytes, wr_buf=4096, in_chunk=1000):
+    """impl_base<true>::deflate called until it returns false (fin)."""
+    frames = []
+    src = ctypes.create_string_buffer(msg, len(msg)) if msg else None
+    consumed = 0
+    while True:
+        out = ctypes.create_string_buffer(wr_buf)
+        zs = ZParams(None, 0, 0, ctypes.cast(out, ctypes.c_void_p), wr_buf, 0, 2)
+        # feed the (remaining) buffers with Flush::none
+        while consumed + zs.total_in < len(msg):
+            at = consumed + zs.total_in
+            k = min(in_chunk, len(msg) - at)
+            zs.next_in = ctypes.addressof(src) + at
+            zs.avail_in = k
+            before = zs.total_in
+            r = L.bpmd_deflate_stream_write(zo, ctypes.byref(zs), NONE)
+            if r != 0:
+                assert r == 1 and zs.avail_out == 0
+                break
+            if zs.avail_out == 0:
+                break
+            assert zs.total_in - before == k
+        consumed += zs.total_in
+        more = True
+        if zs.avail_out > 0 and consumed == len(msg):
+            r = L.bpmd_deflate_stream_write(zo, ctypes.byref(zs), BLOCK)
+            assert r in (0, 1)
+            if zs.avail_out >= 6:
+                r = L.bpmd_deflate_stream_write(zo, ctypes.byref(zs), SYNC)
+                assert r == 0
+                frames.append(out.raw[: zs.total_out - 4])
+                assert out.raw[zs.total_out - 4: zs.total_out] == b"\x00\x00\xff\xff"
+                more = False
+        if more:
+            frames.append(out.raw[: zs.total_out])
+        else:
+            break
+    return b"".join(frames)
+
+
+def ws_inflate_message(L, zi, payload: bytes, user_buf=4096, rd_buf=1536):
+    """read_some's inflate branch: rd_buf slices with Flush::sync, then the
+    00 00 FF FF tail via inflate_with_eb until a call produces nothing."""
+    out = bytearray()
+    pos = 0
+    src = ctypes.create_string_buffer(payload, max(1, len(payload)))
+    while pos < len(payload):
+        buf = ctypes.create_string_buffer(user_buf)
+        k = min(rd_buf, len(payload) - pos)
+        zs = ZParams(ctypes.addressof(src) + pos, k, 0, ctypes.cast(buf, ctypes.c_void_p), user_buf, 0, 2)
+        r = L.bpmd_inflate_stream_write(zi, ctypes.byref(zs), SYNC)
+        assert r in (0, 1), r
+        pos += zs.total_in
+        out += buf.raw[: zs.total_out]
+    eb = ctypes.create_string_buffer(b"\x00\x00\xff\xff", 4)
+    eb_used = 0
+    while True:
+        buf = ctypes.create_string_buffer(user_buf)
+        zs = ZParams(ctypes.addressof(eb) + eb_used, 4 - eb_used, 0, ctypes.cast(buf, ctypes.c_void_p), user_buf, 0, 2)
+        r = L.bpmd_inflate_stream_write(zi, ctypes.byref(zs), SYNC)
+        assert r in (0, 1), r
+        eb_used += zs.total_in
+        out += buf.raw[: zs.total_out]
+        if zs.total_out == 0:
+            break
+    return bytes(out)
+
+
+@pytest.mark.parametrize("size", [0, 1, 100, 4096, 5000, 20000, 70000])
+def test_websocket_message_roundtrip_through_stream_api(size):
+    from beast_amd import pmd
+    L = _lib()
+    zo, zi = _mk(L, True), _mk(L, False)
+    try:
+        for kind in ("json", "binary"):
+            d, _, _ = synth.make_batch(kind, [size], seed=size + 3)
+            msg = bytes(d[:size])
+            payload = ws_deflate_message(L, zo, msg)
+            L.bpmd_deflate_stream_reset(zo)    # do_context_takeover_write (no_context_takeover)
+            # same bytes as the batch kernel
+            res = pmd.deflate_batch(pmd.Batch.from_host([msg]), level=6)
+            assert payload == res.out.to_host()[0]
+            st, back = O.pmd_inflate(payload, cap=max(size, 1))
+            assert st == 0 and back == msg
+            got = ws_inflate_message(L, zi, payload)
+            assert got == msg
+            L.bpmd_inflate_stream_reset(zi, 15)
+    finally:
+        L.bpmd_stream_destroy(zo)
+        L.bpmd_stream_destroy(zi)
+
+
+def test_small_write_buffer_spans_frames():
+    L = _lib()
+    zo = _mk(L, True)
+    d, _, _ = synth.make_batch("random", [9000], seed=1)
+    msg = bytes(d[:9000])
+    payload = ws_deflate_message(L, zo, msg, wr_buf=700, in_chunk=333)
+    st, back = O.pmd_inflate(payload, cap=9000)
+    assert st == 0 and back == msg
+    L.bpmd_stream_destroy(zo)
+
+
+def test_flush_semantics():
+    L = _lib()
+    zo = _mk(L, True)
+    out = ctypes.create_string_buffer(64)
+    zs = ZParams(None, 0, 0, ctypes.cast(out, ctypes.c_void_p), 64, 0, 2)
+    assert L.bpmd_deflate_stream_write(zo, ctypes.byref(zs), SYNC) == 0       # empty stored block
+    assert out.raw[: zs.total_out] == b"\x00\x00\x00\xff\xff"
+    assert L.bpmd_deflate_stream_write(zo, ctypes.byref(zs), SYNC) == 1       # duplicate flush
+    msg = b"hello hello hello"
+    src = ctypes.create_string_buffer(msg, len(msg))
+    zs.next_in, zs.avail_in = ctypes.addressof(src), len(msg)
+    assert L.bpmd_deflate_stream_write(zo, ctypes.byref(zs), FINISH) == 2     # end_of_stream
+    assert L.bpmd_deflate_stream_write(zo, ctypes.byref(zs), SYNC) == 4       # stream_error after finish
+    st, back = O.pmd_inflate(out.raw[: zs.total_out], cap=64, raw=True)
+    assert O.ERRORS[st] == "end_of_stream" and back == msg
+    L.bpmd_stream_destroy(zo)
+
+
+def test_inflate_errors_reported():
+    L = _lib()
+    zi = _mk(L, False)
+    bad = bytes([0x06])   # BTYPE 11: invalid block type
+    src = ctypes.create_string_buffer(bad, 1)
+    out = ctypes.create_string_buffer(16)
+    zs = ZParams(ctypes.addressof(src), 1, 0, ctypes.cast(out, ctypes.c_void_p), 16, 0, 2)
+    assert O.ERRORS[L.bpmd_inflate_stream_write(zi, ctypes.byref(zs), SYNC)] == "invalid_block_type"
+    L.bpmd_stream_destroy(zi)

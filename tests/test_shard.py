@@ -1,0 +1,82 @@
+"""CPU: multi-rank sharding of a message batch (byte-balanced contiguous
+ranges, no payload exchange) and the control-plane collectives, exercised
+with the gloo backend at world_size 2 -- the same code runs over RCCL on
+GPUs in bench.py."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from beast_amd import shard, synth
+from oracle import oracle as O
+
+
+def test_ranges_cover_and_balance_bytes():
+    rng = np.random.default_rng(1)
+    r = np.arange(1, 257)
+    p = r ** -1.1
+    p /= p.sum()
+    lens = 256 * rng.choice(r, size=20000, p=p)    # C4-style Zipf sizes
+    for world in (1, 2, 3, 4, 8):
+        rs = shard.byte_balanced_ranges(lens, world)
+        assert rs[0][0] == 0 and rs[-1][1] == len(lens)
+        assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
+        b = [int(lens[s:e].sum()) for s, e in rs]
+        assert max(b) - min(b) <= 2 * int(lens.max()), b
+
+
+def test_ranges_degenerate():
+    assert shard.byte_balanced_ranges(np.array([], dtype=np.int64), 4) == [(0, 0)] * 4
+    rs = shard.byte_balanced_ranges(np.array([5, 0, 0]), 2)
+    assert rs[0][0] == 0 and rs[-1][1] == 3
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lens = np.array([100, 4096, 17, 9000, 0, 2500, 4096, 333], dtype=np.uint32)
+    data, off, ln = synth.make_batch("json", lens, seed=9)
+    rs = shard.byte_balanced_ranges(ln, world)
+    d, o, l = shard.local_slice(data, off, ln, rs[rank])
+    # each rank compresses only its own messages (the CPU oracle stands in
+    # for the device here; this test covers the partitioning and collectives)
+    local = [O.pmd_deflate(bytes(d[int(o[i]):int(o[i]) + int(l[i])]), 6, 15, 4) for i in range(len(l))]
+    start, total = shard.global_output_offsets(sum(len(x) for x in local))
+    t = shard.max_over_ranks(float(rank + 1))
+    q.put((rank, rs[rank], start, total, t, b"".join(local)))
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_shards_and_collectives():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    lens = np.array([100, 4096, 17, 9000, 0, 2500, 4096, 333], dtype=np.uint32)
+    data, off, ln = synth.make_batch("json", lens, seed=9)
+    expect = b"".join(O.pmd_deflate(bytes(data[int(off[i]):int(off[i]) + int(ln[i])]), 6, 15, 4)
+                      for i in range(len(ln)))
+    # ranges partition the batch, offsets place rank outputs back to back
+    assert res[0][1][0] == 0 and res[0][1][1] == res[1][1][0] and res[1][1][1] == len(ln)
+    assert res[0][2] == 0 and res[1][2] == len(res[0][5]) and res[0][3] == res[1][3] == len(expect)
+    assert res[0][5] + res[1][5] == expect
+    assert res[0][4] == res[1][4] == 2.0
