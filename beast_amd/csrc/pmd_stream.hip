@@ -280,6 +280,44 @@ extern "C" int bpmd_deflate_stream_write(bpmd_stream* s, bpmd_zparams* zs, int f
     return BPMD_OK;
 }
 
+extern "C" int bpmd_deflate_stream_params(bpmd_stream* s, bpmd_zparams* zs, int level, int strategy)
+{
+    // deflate_stream::params (deflate_stream.ipp:307-338): buffered input is
+    // compressed with the old parameters first, as a Flush::block
+    if (!s || !s->is_deflate || !zs) return BPMD_R_INVALID_ARGUMENT;
+    if (level == -1) level = 6;
+    if (level < 0 || level > 9 || strategy < BPMD_STRATEGY_NORMAL || strategy > BPMD_STRATEGY_FIXED)
+        return BPMD_STREAM_ERROR;
+    int r = BPMD_OK;
+    if (!s->in.empty() && (level != s->level || strategy != s->strategy)) {
+        r = bpmd_deflate_stream_write(s, zs, BPMD_FLUSH_BLOCK);
+        if (r == BPMD_NEED_BUFFERS) r = BPMD_OK;
+    }
+    if (r == BPMD_OK) {
+        s->level = level;
+        s->strategy = strategy;
+    }
+    return r;
+}
+
+extern "C" int bpmd_deflate_stream_pending(bpmd_stream* s, unsigned* value, int* bits)
+{
+    // deflate_stream::pending (deflate_stream.hpp:344-348)
+    if (!s || !s->is_deflate) return BPMD_R_INVALID_ARGUMENT;
+    if (value) *value = (unsigned)(s->pend.size() - s->pend_pos);
+    if (bits) *bits = (int)s->nbits;
+    return BPMD_OK;
+}
+
+extern "C" int bpmd_deflate_stream_prime(bpmd_stream* s, int bits, int value)
+{
+    // deflate_stream::prime (deflate_stream.ipp:340-355): insert up to 16 bits
+    if (!s || !s->is_deflate) return BPMD_R_INVALID_ARGUMENT;
+    if (bits < 0 || bits > 16) return BPMD_NEED_BUFFERS;
+    if (bits) put_bits(s, (uint32_t)value & ((1u << bits) - 1u), (unsigned)bits);
+    return BPMD_OK;
+}
+
 extern "C" int bpmd_inflate_stream_create(int window_bits, bpmd_stream** out)
 {
     if (!out) return BPMD_R_INVALID_ARGUMENT;

@@ -156,6 +156,12 @@ int bpmd_deflate_stream_reset(bpmd_stream* s);
 /* deflate_stream::write(zs, flush, ec) (deflate_stream.ipp:357-499): returns
  * the zlib::error value (0 = none) or BPMD_R_INVALID_ARGUMENT where it throws */
 int bpmd_deflate_stream_write(bpmd_stream* s, bpmd_zparams* zs, int flush);
+/* deflate_stream::params(zs, level, strategy, ec) (deflate_stream.ipp:307-338) */
+int bpmd_deflate_stream_params(bpmd_stream* s, bpmd_zparams* zs, int level, int strategy);
+/* deflate_stream::pending(value, bits) (deflate_stream.hpp:344-348) */
+int bpmd_deflate_stream_pending(bpmd_stream* s, unsigned* value, int* bits);
+/* deflate_stream::prime(bits, value, ec) (deflate_stream.ipp:340-355) */
+int bpmd_deflate_stream_prime(bpmd_stream* s, int bits, int value);
 /* inflate_stream::reset(windowBits) (inflate_stream.ipp:55-72);
  * BPMD_R_DOMAIN_ERROR where it throws */
 int bpmd_inflate_stream_create(int window_bits, bpmd_stream** out);
