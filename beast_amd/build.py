@@ -50,6 +50,9 @@ def build(verbose: bool = False, variant: str = "") -> str:
     bdir = BUILD + (f"_{variant}" if variant else "")
     lib = LIB.replace(".so", f"_{variant}.so") if variant else LIB
     extra = ("-DBPMD_PROF",) if variant == "prof" else ()
+    # experiment variants: BPMD_EXTRA_FLAGS="-DBPMD_RING=8192 ..." python build.py <name>
+    if variant and variant != "prof":
+        extra = tuple(os.environ.get("BPMD_EXTRA_FLAGS", "").split())
     os.makedirs(bdir, exist_ok=True)
     hmt = _headers_mtime()
     srcs = _sources()

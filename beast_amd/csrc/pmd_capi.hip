@@ -24,6 +24,11 @@ int g_init_device = -1;   // device whose symbols are initialised
 
 extern "C" const char* bpmd_version(void) { return "beast_pmd 0.1 (gfx950)"; }
 
+// Diagnostics only (scripts/diag_*.py): force the launch grid, e.g. one
+// wave, to time a kernel's phases without other waves on the CU.
+extern "C" unsigned bpmd_diag_grid_override = 0;
+extern "C" void bpmd_diag_set_grid(unsigned grid) { bpmd_diag_grid_override = grid; }
+
 extern "C" int bpmd_init(void)
 {
     int dev = -1;

@@ -1045,6 +1045,8 @@ deflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
 }  // namespace dfl
 }  // namespace bpmd
 
+extern "C" unsigned bpmd_diag_grid_override;   // pmd_capi.hip; 0 = size the grid by occupancy
+
 namespace {
 template <int HIST>
 int launch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n, uint8_t* out,
@@ -1055,6 +1057,7 @@ int launch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, ui
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const unsigned per_cu = (160u * 1024u) / (unsigned)sizeof(bpmd::dfl::DefLds<HIST>);
     unsigned grid = (unsigned)cus * (per_cu ? per_cu : 1u);
+    if (bpmd_diag_grid_override) grid = bpmd_diag_grid_override;
     if (grid > n) grid = n;
     hipLaunchKernelGGL(bpmd::dfl::deflate_kernel<HIST>, dim3(grid), dim3(64), 0, stream, in, in_off, in_len, n, out,
                        out_off, out_cap, out_len, status, P);

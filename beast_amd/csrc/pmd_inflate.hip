@@ -40,14 +40,27 @@
 
 namespace bpmd {
 
-constexpr unsigned RING = 8192;          // output history ring (bytes)
+#ifndef BPMD_RING
+#define BPMD_RING 4096
+#endif
+#ifndef BPMD_TOT
+#define BPMD_TOT 1024
+#endif
+// LDS per wave bounds the waves per CU, and the decode passes are latency
+// bound (one wave alone runs its phases at the same speed as six sharing a
+// CU), so the ring and token list are sized for occupancy: a 4 KiB ring and
+// 1024 tokens per round still hold a whole 1023-symbol zlib block of text.
+constexpr unsigned RING = BPMD_RING;     // output history ring (bytes)
 constexpr unsigned RING_MASK = RING - 1;
 constexpr unsigned R_MAX = RING - 256;   // output bytes per round, at most
 constexpr unsigned IN_CAP = 2560;        // input window bytes
 constexpr unsigned IN_PAD = 32;
 constexpr unsigned WIN_WORDS = (IN_CAP + IN_PAD) / 4;
-constexpr unsigned TOT = 2048;           // tokens per round, at most
-constexpr unsigned SEG_TOKENS = 32;      // target tokens per lane segment
+constexpr unsigned TOT = BPMD_TOT;       // tokens per round, at most
+#ifndef BPMD_SEG_TOKENS
+#define BPMD_SEG_TOKENS 32
+#endif
+constexpr unsigned SEG_TOKENS = BPMD_SEG_TOKENS;   // target tokens per lane segment
 constexpr unsigned SEG_MAX_BITS = 300;   // keeps a round inside the window
 constexpr unsigned BM_WORDS = (R_MAX + 128) / 32 + 2;
 
@@ -820,6 +833,8 @@ inflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
 
 // ---------------------------------------------------------------- launcher
 
+extern "C" unsigned bpmd_diag_grid_override;   // pmd_capi.hip; 0 = size the grid by occupancy
+
 extern "C" int bpmd_internal_inflate(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n,
                                      uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                                      uint32_t* out_len, int32_t* status, uint32_t raw, hipStream_t stream)
@@ -831,6 +846,7 @@ extern "C" int bpmd_internal_inflate(const uint8_t* in, const uint64_t* in_off, 
     const size_t lds = sizeof(WaveLds);
     const unsigned per_cu = (unsigned)(160 * 1024 / lds);
     unsigned grid = (unsigned)cus * (per_cu ? per_cu : 1);
+    if (bpmd_diag_grid_override) grid = bpmd_diag_grid_override;
     if (grid > n) grid = n;
     hipLaunchKernelGGL(inflate_kernel, dim3(grid), dim3(WAVE), lds, stream, in, in_off, in_len, n, out, out_off,
                        out_cap, out_len, status, raw);

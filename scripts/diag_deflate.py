@@ -32,6 +32,8 @@ def main():
     src = pmd.Batch.from_arrays(raw, off.astype(np.int64), ln.astype(np.int32))
     L = pmd.lib()
     L.bpmd_diag_deflate_counters.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    L.bpmd_diag_set_grid.argtypes = [ctypes.c_uint]
+    L.bpmd_diag_set_grid(int(os.environ.get("DIAG_GRID", "0")))
     c = (ctypes.c_ulonglong * 24)()
     pmd.deflate_batch(src, level=level)
     torch.cuda.synchronize()

@@ -34,6 +34,8 @@ def main():
     src = pmd.Batch(torch.from_numpy(buf).to(dev), torch.from_numpy(coff).to(dev), torch.from_numpy(clen).to(dev))
     L = pmd.lib()
     L.bpmd_diag_counters.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    L.bpmd_diag_set_grid.argtypes = [ctypes.c_uint]
+    L.bpmd_diag_set_grid(int(os.environ.get("DIAG_GRID", "0")))
     c = (ctypes.c_ulonglong * 24)()
     r = pmd.inflate_batch(src, size)
     torch.cuda.synchronize()
