@@ -58,7 +58,7 @@ constexpr unsigned IN_PAD = 32;
 constexpr unsigned WIN_WORDS = (IN_CAP + IN_PAD) / 4;
 constexpr unsigned TOT = BPMD_TOT;       // tokens per round, at most
 #ifndef BPMD_SEG_TOKENS
-#define BPMD_SEG_TOKENS 32
+#define BPMD_SEG_TOKENS 20
 #endif
 constexpr unsigned SEG_TOKENS = BPMD_SEG_TOKENS;   // target tokens per lane segment
 constexpr unsigned SEG_MAX_BITS = 300;   // keeps a round inside the window
