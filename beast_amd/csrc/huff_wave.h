@@ -206,7 +206,7 @@ __device__ int build_table_wave(const uint8_t* lens, unsigned n, uint16_t* tab, 
 #pragma unroll
             for (unsigned d = 1; d < 64; d <<= 1) {
                 const uint32_t y = __shfl_up(incl, d);
-                if (lane >= d) incl += y;
+                incl += lane >= d ? y : 0u;   // select: a shuffle must not sink under divergence
             }
             const uint32_t off = carry_off + incl - size;   // same for every code of a group
             const uint64_t sm = __ballot(start);

@@ -78,3 +78,35 @@ extern "C" int bpmd_diag_build_tables(const uint8_t* d_lens, const uint32_t* d_n
                        count, d_wave, d_serial, d_meta);
     return (int)hipGetLastError();
 }
+
+// Self-check of the pointer-doubling chain finder used by the inflate
+// kernel's code-length decode: step[c*64 + lane] -> chain mask of case c.
+__global__ void __launch_bounds__(64) diag_chain_kernel(const uint32_t* steps, uint32_t count, uint64_t* out)
+{
+    const unsigned lane = bpmd::lane_id();
+    for (uint32_t c = blockIdx.x; c < count; c += gridDim.x) {
+        const uint32_t step = steps[c * 64 + lane];
+        uint32_t J = lane + step;
+        uint64_t R = (1ull << lane) | (J < 64 ? (1ull << J) : 0ull);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const uint32_t jj = J < 64 ? J : lane;
+            const uint32_t rlo = __shfl((uint32_t)R, jj), rhi = __shfl((uint32_t)(R >> 32), jj);
+            const uint32_t j2 = __shfl(J, jj);
+            const uint64_t keep = J < 64 ? ~0ull : 0ull;
+            R |= (((uint64_t)rhi << 32) | rlo) & keep;
+            J = J < 64 ? j2 : J;
+        }
+        const uint64_t chain = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(R >> 32)) << 32) |
+                               (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)R);
+        if (lane == 0) out[c] = chain;
+    }
+}
+
+extern "C" int bpmd_diag_chain(const uint32_t* d_steps, uint32_t count, uint64_t* d_out, void* stream)
+{
+    if (count == 0) return 0;
+    hipLaunchKernelGGL(diag_chain_kernel, dim3(count < 1024 ? count : 1024), dim3(64), 0, (hipStream_t)stream,
+                       d_steps, count, d_out);
+    return (int)hipGetLastError();
+}

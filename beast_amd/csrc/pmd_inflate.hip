@@ -362,7 +362,7 @@ __device__ __forceinline__ uint32_t scan_incl(uint32_t x)
 #pragma unroll
     for (unsigned d = 1; d < WAVE; d <<= 1) {
         const uint32_t y = __shfl_up(x, d);
-        if (lane >= d) x += y;
+        x += lane >= d ? y : 0u;   // select: a shuffle must not sink under divergence
     }
     return x;
 }
@@ -574,50 +574,90 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
             wave_sync();
             unsigned have = 0, prevlen = 0;
             while (have < want) {
+                // Every lane decodes the symbol that would start at bit w +
+                // lane; the true chain from w is found by pointer doubling
+                // over reach masks, then the chain members are processed in
+                // order with prefix sums -- the reference's per-symbol checks
+                // (ipp:264-327) become "first member with an event".
                 const uint32_t w = pos;
                 const uint64_t v = peek64(L.win, w + lane - wbase * 8);
                 const uint16_t s = L.tab[lowbits(v, croot)];
                 const unsigned sym = slot_val(s), cb = slot_bits(s);
                 const unsigned xb = sym < 16 ? 0u : (sym == 16 ? 2u : sym == 17 ? 3u : 7u);
                 const unsigned x = lowbits(v >> cb, xb);
-                const uint32_t packed = (cb + xb) | (sym << 5) | (x << 10) | (cb << 17);
-                uint32_t cur = w;
-                // run starts found in this window: (position << 8) | (value + 1),
-                // collected in lane order with v_writelane, stored once
-                uint32_t marks = 0;
-                unsigned nmarks = 0;
-                while (cur < w + WAVE && have < want) {
-                    const uint32_t pk = __builtin_amdgcn_readlane(packed, cur - w);
-                    const unsigned tb = pk & 31, sy = (pk >> 5) & 31, xx = (pk >> 10) & 127, c0 = (pk >> 17) & 15;
-                    const uint32_t av = total_bits - cur;
-                    if (av < croot) { starved = true; break; }
-                    unsigned rep, val;
-                    if (sy < 16) {
-                        rep = 1;
-                        val = sy;
-                        cur += c0;
-                    } else {
-                        // code and extra bits are asked for together (ipp:282-312)
-                        if (av < tb) { starved = true; break; }
-                        if (sy == 16) {
-                            if (have == 0) { st = ST_INVALID_BIT_LENGTH_REPEAT; break; }
-                            rep = 3 + xx;
-                            val = prevlen;
-                        } else {
-                            rep = (sy == 17 ? 3 : 11) + xx;
-                            val = 0;
-                        }
-                        if (have + rep > want) { st = ST_INVALID_BIT_LENGTH_REPEAT; break; }
-                        cur += tb;
-                    }
-                    marks = lane == nmarks ? ((have << 8) | (val + 1)) : marks;
-                    ++nmarks;
-                    have += rep;
-                    prevlen = val;
+                const unsigned step = sym < 16 ? cb : cb + xb;
+                // reach masks: R(o) = positions of the window reachable from o
+                uint32_t J = lane + step;   // successor (>= 64: leaves the window)
+                uint64_t R = (1ull << lane) | (J < WAVE ? (1ull << J) : 0ull);
+#pragma unroll
+                for (int k = 0; k < 6; ++k) {
+                    const uint32_t jj = J < WAVE ? J : lane;
+                    const uint32_t rlo = __shfl((uint32_t)R, jj), rhi = __shfl((uint32_t)(R >> 32), jj);
+                    const uint32_t j2 = __shfl(J, jj);
+                    // selects, not a branch: a shuffle sunk under divergence
+                    // would read 0 from the switched-off lanes
+                    const uint64_t keep = J < WAVE ? ~0ull : 0ull;
+                    R |= (((uint64_t)rhi << 32) | rlo) & keep;
+                    J = J < WAVE ? j2 : J;
                 }
-                if (lane < nmarks) L.u.h.runval[marks >> 8] = (uint8_t)(marks & 0xff);
-                pos = cur;
-                if (st || starved) break;
+                const uint64_t chain = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(R >> 32)) << 32) |
+                                       (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)R);   // returns int: no sign extension
+                const bool mem = (chain >> lane) & 1;
+                const unsigned rep = !mem ? 0u : sym < 16 ? 1u : sym == 16 ? 3u + x : (sym == 17 ? 3u : 11u) + x;
+                const uint32_t incl = scan_incl(rep);
+                const uint32_t hb = have + incl - rep;       // lengths decoded before this member
+                const uint32_t av = total_bits - (w + lane);
+                // events in the reference's order: starved (root bits, then
+                // code + extra together), repeat without a previous length,
+                // repeat past the end
+                const unsigned ev = !mem ? 0u
+                                  : av < croot ? 1u
+                                  : sym < 16 ? 0u
+                                  : av < cb + xb ? 1u
+                                  : (sym == 16 && hb == 0) ? 2u
+                                  : hb + rep > want ? 2u : 0u;
+                const uint64_t m_done = __ballot(mem && hb >= want);
+                const uint64_t m_ev = __ballot(ev != 0);
+                const unsigned f_done = first_lane(m_done), f_ev = first_lane(m_ev);
+                const unsigned stop_at = f_done < f_ev ? f_done : f_ev;   // first member not processed
+                const bool proc = mem && lane < stop_at;
+                // value of a repeat (16) = the last earlier non-16 member's
+                const unsigned own = sym < 16 ? sym : 0u;
+                const uint32_t src = (proc && sym != 16) ? lane + 1 : 0u;
+                uint32_t lastsrc = src;
+#pragma unroll
+                for (unsigned d = 1; d < WAVE; d <<= 1) {
+                    const uint32_t y = __shfl_up(lastsrc, d);
+                    lastsrc = (lane >= d && y > lastsrc) ? y : lastsrc;
+                }
+                const uint32_t from = lastsrc ? lastsrc - 1 : 0u;
+                const uint32_t vfrom = __shfl(own, from);
+                const unsigned val = sym == 16 ? (lastsrc ? vfrom : prevlen) : own;
+                if (proc) L.u.h.runval[hb] = (uint8_t)(val + 1);
+                const uint64_t pm = __ballot(proc);
+#ifdef BPMD_PROF
+                const uint32_t have_in = have;
+#endif
+                if (pm) {
+                    const unsigned lastp = 63u - (unsigned)__builtin_clzll(pm);
+                    have = __shfl(hb + rep, lastp);
+                    prevlen = __shfl(val, lastp);
+                    pos = w + __shfl(lane + step, lastp);
+                }
+#ifdef BPMD_PROF
+                if (lane == 0 && g_prof_dbg[15] < 5) {
+                    const unsigned k5 = (unsigned)g_prof_dbg[15];
+                    g_prof_dbg[3 * k5] = chain;
+                    g_prof_dbg[3 * k5 + 1] = ((unsigned long long)have_in << 32) | have;
+                    g_prof_dbg[3 * k5 + 2] = ((unsigned long long)stop_at << 32) | (63u - (unsigned)__builtin_clzll(pm | 1));
+                    g_prof_dbg[15] = k5 + 1;
+                }
+#endif
+                if (f_ev < f_done) {
+                    if (__shfl(ev, f_ev) == 1) starved = true;
+                    else st = ST_INVALID_BIT_LENGTH_REPEAT;
+                    break;
+                }
             }
             if (st) break;
             if (starved) break;

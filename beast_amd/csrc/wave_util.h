@@ -32,7 +32,7 @@ __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x)
 #pragma unroll
     for (unsigned d = 1; d < WAVE; d <<= 1) {
         const uint32_t y = __shfl_up(x, d);
-        if (lane >= d) x += y;
+        x += lane >= d ? y : 0u;   // select: a shuffle must not sink under divergence
     }
     return x;
 }
@@ -44,7 +44,7 @@ __device__ __forceinline__ uint32_t wave_scan_max_excl(uint32_t x, uint32_t iden
 #pragma unroll
     for (unsigned d = 1; d < WAVE; d <<= 1) {
         const uint32_t y = __shfl_up(x, d);
-        if (lane >= d) x = x > y ? x : y;
+        x = (lane >= d && y > x) ? y : x;
     }
     const uint32_t e = __shfl_up(x, 1);
     return lane == 0 ? ident : (e > ident ? e : ident);
