@@ -1,6 +1,9 @@
 // pmd_capi.hip -- extern "C" entry points declared in include/beast_pmd.h.
 #include <hip/hip_runtime.h>
 
+#include <stdlib.h>
+#include <string.h>
+
 #include <atomic>
 #include <mutex>
 
@@ -11,6 +14,12 @@ extern "C" int bpmd_internal_inflate(const uint8_t* in, const uint64_t* in_off, 
                                         uint32_t n, uint8_t* out, const uint64_t* out_off,
                                         const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
                                         uint32_t raw, hipStream_t stream);
+
+extern "C" int bpmd_internal_init_fixed_lane(void);
+extern "C" int bpmd_internal_inflate_lane(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                          uint32_t n, uint8_t* out, const uint64_t* out_off,
+                                          const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
+                                          uint32_t raw, hipStream_t stream);
 
 extern "C" int bpmd_internal_deflate(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                      uint32_t n, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
@@ -29,6 +38,31 @@ extern "C" const char* bpmd_version(void) { return "beast_pmd 0.1 (gfx950)"; }
 extern "C" unsigned bpmd_diag_grid_override = 0;
 extern "C" void bpmd_diag_set_grid(unsigned grid) { bpmd_diag_grid_override = grid; }
 
+// Kernel choice for a batch: one lane per message (pmd_inflate_lane.hip)
+// for throughput, one wave per message (pmd_inflate.hip) for latency when
+// the batch is too small to fill the chip's lanes.  BPMD_INFLATE=lane|wave
+// or bpmd_set_inflate_kernel() forces one (the tests run both).
+static std::atomic<int> g_inflate_kernel{-1};   // -1 unset, 0 auto, 1 lane, 2 wave
+
+extern "C" int bpmd_set_inflate_kernel(int mode)
+{
+    if (mode < 0 || mode > 2) return BPMD_R_INVALID_ARGUMENT;
+    g_inflate_kernel.store(mode);
+    return BPMD_R_OK;
+}
+
+static bool inflate_use_lane(uint32_t n)
+{
+    int m = g_inflate_kernel.load();
+    if (m < 0) {
+        const char* e = getenv("BPMD_INFLATE");
+        m = (e && !strcmp(e, "lane")) ? 1 : (e && !strcmp(e, "wave")) ? 2 : 0;
+        g_inflate_kernel.store(m);
+    }
+    if (m) return m == 1;
+    return n >= 2048;
+}
+
 extern "C" int bpmd_init(void)
 {
     int dev = -1;
@@ -38,6 +72,7 @@ extern "C" int bpmd_init(void)
     std::lock_guard<std::mutex> lk(g_init_mu);
     if (g_init_device == dev) return BPMD_R_OK;
     if (bpmd_internal_init_fixed() != 0) return BPMD_R_HIP_ERROR;
+    if (bpmd_internal_init_fixed_lane() != 0) return BPMD_R_HIP_ERROR;
     g_init_device = dev;
     return BPMD_R_OK;
 }
@@ -61,8 +96,12 @@ extern "C" int bpmd_inflate_batch(const bpmd_cfg* cfg, const uint8_t* d_in, cons
         return BPMD_R_INVALID_ARGUMENT;
     int r = bpmd_init();
     if (r) return r;
-    int e = bpmd_internal_inflate(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
-                                     d_status, (cfg->flags & BPMD_F_RAW) ? 1u : 0u, (hipStream_t)stream);
+    const uint32_t raw = (cfg->flags & BPMD_F_RAW) ? 1u : 0u;
+    int e = inflate_use_lane(n_msgs)
+                ? bpmd_internal_inflate_lane(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
+                                             d_status, raw, (hipStream_t)stream)
+                : bpmd_internal_inflate(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
+                                        d_status, raw, (hipStream_t)stream);
     return e ? BPMD_R_HIP_ERROR : BPMD_R_OK;
 }
 

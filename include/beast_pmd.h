@@ -117,6 +117,13 @@ int bpmd_deflate_batch(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t*
                        const uint64_t* d_out_off, const uint32_t* d_out_cap,
                        uint32_t* d_out_len, int32_t* d_status, void* stream);
 
+/* Inflate kernel selection (no reference counterpart; tuning and tests):
+ * 0 automatic (one lane per message for batches of >= 2048 messages, one
+ * wave per message below), 1 always lane-per-message, 2 always
+ * wave-per-message.  Both produce identical results.  Initial value from
+ * the BPMD_INFLATE environment variable ("lane" / "wave"). */
+int bpmd_set_inflate_kernel(int mode);
+
 /* deflate_upper_bound (zlib/deflate_stream.hpp:402-410): size a d_out slot. */
 size_t bpmd_deflate_upper_bound(size_t n);
 

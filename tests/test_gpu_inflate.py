@@ -14,6 +14,17 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 
+@pytest.fixture(autouse=True, params=["lane", "wave"])
+def inflate_kernel(request):
+    """Every inflate test runs on both kernels (pmd_inflate_lane.hip and
+    pmd_inflate.hip), forced through bpmd_set_inflate_kernel."""
+    pmd = _pmd()
+    mode = {"lane": 1, "wave": 2}[request.param]
+    assert pmd.lib().bpmd_set_inflate_kernel(mode) == 0
+    yield request.param
+    pmd.lib().bpmd_set_inflate_kernel(0)
+
+
 def _pmd():
     import torch  # noqa: F401
     from beast_amd import pmd
