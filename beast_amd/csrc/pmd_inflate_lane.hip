@@ -138,13 +138,97 @@ __device__ __forceinline__ uint4 load_block(const uint8_t* A, uint32_t bi, uint3
 
 typedef uint4 uint4_u __attribute__((aligned(1)));
 typedef uint2 uint2_u __attribute__((aligned(1)));
-typedef uint64_t u64_u __attribute__((aligned(1)));
+
+// Reads of the lane's own earlier output (match sources).  The vector L1 is
+// not updated by this CU's stores, so a line it cached from an earlier read
+// of the slot could return bytes written since; these reads use the sc1
+// (agent-coherent) policy, which fetches from L2.  Normally one buffer
+// resource based at the wave's lowest slot; if the wave's slots span 4 GiB
+// or more, aligned relaxed agent-scope atomic loads do the same job.
+struct Hist {
+    __amdgpu_buffer_rsrc_t r;
+    uint32_t vb;   // this lane's slot, as an offset from the resource base
+    bool buf;      // wave-uniform
+};
+constexpr int kSc1 = 16;
+
+__device__ __forceinline__ uint64_t aload64(const uint8_t* a)
+{
+    return __hip_atomic_load((const uint64_t*)a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// 8 bytes at o + off (off need not be aligned); every word read lies inside
+// [o + off - 7, o + off + 16)
+__device__ __forceinline__ uint64_t hread8(const Hist& h, const uint8_t* o, uint32_t off)
+{
+    if (h.buf) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(h.r, h.vb + off, 0, kSc1);
+        return ((uint64_t)v[1] << 32) | v[0];
+    }
+    const uint8_t* a = o + off;
+    const uint8_t* al = a - ((uintptr_t)a & 7);
+    const unsigned sh = (unsigned)((uintptr_t)a & 7) * 8;
+    const uint64_t lo = aload64(al);
+    if (!sh) return lo;
+    return (lo >> sh) | (aload64(al + 8) << (64 - sh));
+}
+__device__ __forceinline__ uint4 hread16(const Hist& h, const uint8_t* o, uint32_t off)
+{
+    if (h.buf) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(h.r, h.vb + off, 0, kSc1);
+        return make_uint4(v[0], v[1], v[2], v[3]);
+    }
+    const uint64_t a = hread8(h, o, off), b = hread8(h, o, off + 8);
+    return make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+}
+__device__ __forceinline__ uint32_t hread1(const Hist& h, const uint8_t* o, uint32_t off)
+{
+    if (h.buf) return __builtin_amdgcn_raw_buffer_load_b8(h.r, h.vb + off, 0, kSc1);
+    const uint8_t* a = o + off;
+    const uint32_t* w = (const uint32_t*)(a - ((uintptr_t)a & 3));
+    const uint32_t v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return (v >> (((uintptr_t)a & 3) * 8)) & 0xffu;
+}
+
+__device__ __forceinline__ uint64_t wave_min64(uint64_t x)
+{
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t lo = __shfl_xor((uint32_t)x, d), hi = __shfl_xor((uint32_t)(x >> 32), d);
+        const uint64_t y = ((uint64_t)hi << 32) | lo;
+        x = y < x ? y : x;
+    }
+    return x;
+}
+__device__ __forceinline__ uint64_t wave_max64(uint64_t x)
+{
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t lo = __shfl_xor((uint32_t)x, d), hi = __shfl_xor((uint32_t)(x >> 32), d);
+        const uint64_t y = ((uint64_t)hi << 32) | lo;
+        x = y > x ? y : x;
+    }
+    return x;
+}
 
 static __constant__ const uint8_t kClenOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
 // fixed-code canonical symbol image (low 8 bits): lengths 7: 256-279,
 // 8: 0-143 then 280-287, 9: 144-255; distances 0-31
 __device__ __attribute__((aligned(16))) uint32_t g_fixed_img[80];
+
+// Diagnostic build only (-DBPMD_PROF): per-wave loop counters.
+__device__ unsigned long long g_lprof[16];
+#ifdef BPMD_PROF
+#define LP_DECL unsigned long long lp_[16] = {0}; unsigned long long lpt_ = __builtin_amdgcn_s_memtime(), lpt0_ = lpt_
+#define LP_LAP(i) do { unsigned long long t2_ = __builtin_amdgcn_s_memtime(); lp_[i] += t2_ - lpt_; lpt_ = t2_; } while (0)
+#define LP_CNT(i, n) (lp_[i] += (n))
+#define LP_FLUSH() do { lp_[0] = __builtin_amdgcn_s_memtime() - lpt0_; if (lane == 0) for (int i_ = 0; i_ < 16; ++i_) atomicAdd(&g_lprof[i_], lp_[i_]); } while (0)
+#else
+#define LP_DECL
+#define LP_LAP(i)
+#define LP_CNT(i, n)
+#define LP_FLUSH()
+#endif
 
 __global__ void __launch_bounds__(64)
 inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
@@ -169,19 +253,34 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
         cap = out_cap[msg];
         o = out + out_off[msg];
     }
+    Hist hs;
+    {
+        const uint64_t mo = valid ? out_off[msg] : ~0ull;
+        const uint64_t lo = wave_min64(mo);
+        const uint64_t hi = wave_max64(valid ? mo + cap + 64 : 0ull);
+        hs.buf = hi - lo < 0xffffff00ull;
+        hs.r = __builtin_amdgcn_make_buffer_rsrc(out + (hs.buf ? lo : 0), 0, -1, 0x00020000);
+        hs.vb = valid ? (uint32_t)(mo - lo) : 0u;
+    }
     const uint32_t tail = raw ? 0u : 4u;
     const int32_t full_status = raw ? ST_OK : ST_NEED_BUFFERS;
 
-    // ---- bit reader: 64-bit buffer refilled 32 bits at a time from a
-    // 16-byte block (q) with the next block (r) already in flight.
-    const uint8_t* A = (const uint8_t*)((uintptr_t)p & ~(uintptr_t)3);
+    // ---- bit reader.  bb holds up to 64 bits; refills take 32-bit words
+    // from q (a 16-byte block, shifted down as it is used), then from nx
+    // (the next block, already in registers).  Blocks move nx <- sg <- memory
+    // only in the loop's memory section, so decoding never waits on memory.
+    // (pointer arithmetic, not integer casts, keeps these global_ loads:
+    // flat loads would also count on lgkmcnt and stall every LDS wait)
     const uint32_t s = (uint32_t)((uintptr_t)p & 3);
-    uint4 q = make_uint4(0, 0, 0, 0), r = q;
+    const uint8_t* A = p - s;
+    uint4 q = make_uint4(0, 0, 0, 0), nx = q, sg = q;
     if (valid) {
         q = load_block(A, 0, s, n, tail);
-        r = load_block(A, 1, s, n, tail);
+        nx = load_block(A, 1, s, n, tail);
+        sg = load_block(A, 2, s, n, tail);
     }
-    uint32_t blk = 2, qn = 4;
+    uint32_t blk = 3, qn = 4;
+    bool nx_used = false;   // nx moved into q: refill nx from sg in the next memory section
     uint64_t bb = 0;
     uint32_t nb = 0;
     int32_t tb = (int32_t)(8 * (s + n + tail));   // stream bits not yet moved into bb
@@ -194,9 +293,9 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
             q.y = q.z;
             q.z = q.w;
             if (--qn == 0) {
-                q = r;
+                q = nx;
                 qn = 4;
-                r = load_block(A, blk++, s, n, tail);
+                nx_used = true;
             }
         }
     };
@@ -228,22 +327,121 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
     // stored block
     uint32_t srem = 0;
     bool sfull = false, sstarve = false;
-    // match copy: bytes left, distance, next output position, pattern
+    // match copy: bytes left to issue, distance, next output position
     uint32_t crem = 0, cdist = 0, cq = 0;
     uint64_t cpat = 0;
-    bool cpat_ok = false;
-    // deferred chunk store
-    bool pend = false;
-    uint32_t pdst = 0, psz = 0;
-    uint4 pw = make_uint4(0, 0, 0, 0);
+    uint32_t cpat_st = 0;   // dist < 8: 0 pattern not requested, 1 source bytes in flight, 2 pattern ready
+    // chunk loaded in the previous memory section, stored in the next one
+    bool cst = false, cst_pat = false;
+    uint32_t cdst = 0, csz = 0, cpd = 1;
+    uint4 cw = make_uint4(0, 0, 0, 0);
+    // byte stores decided by the previous compute section (literal or stored-block bytes)
+    uint32_t bcnt = 0, bdst = 0, bval = 0;
 
+    LP_DECL;
     for (;;) {
-        const bool alive = st != S_DONE || crem != 0 || pend;
-        if (!__builtin_amdgcn_ballot_w64(alive)) break;
+        const bool alive = st != S_DONE || crem != 0 || cst || bcnt != 0;
+        const uint64_t alive_m = __builtin_amdgcn_ballot_w64(alive);
+        if (!alive_m) break;
+        LP_CNT(1, 1);
+        LP_CNT(2, __builtin_popcountll(alive_m));
+        LP_CNT(3, __builtin_amdgcn_ballot_w64(st == S_DATA && crem == 0) != 0);
+        LP_CNT(4, __builtin_popcountll(__builtin_amdgcn_ballot_w64(st == S_DATA && crem == 0)));
+        LP_CNT(5, __builtin_amdgcn_ballot_w64(crem != 0) != 0);
+        LP_CNT(6, __builtin_amdgcn_ballot_w64(st != S_DATA && st != S_DONE) != 0);
+        LP_CNT(7, __builtin_popcountll(__builtin_amdgcn_ballot_w64(st != S_DATA && st != S_DONE)));
+        LP_CNT(13, __builtin_amdgcn_ballot_w64(st == S_PASS1) != 0);
+        LP_CNT(14, __builtin_amdgcn_ballot_w64(st == S_PASS2) != 0);
+        LP_LAP(15);
 
-        // ================================================ A. decode a token
-        bool emit_lit = false;
-        uint32_t lit_byte = 0, lit_pos = 0;
+        // ================================================ memory section
+        // Every global load of the loop is issued here and its data is only
+        // used in the next iteration's memory section, so the one wait per
+        // iteration covers loads that had a whole decode step to land.
+        // Stores go in output order (a chunk's spare tail bytes are always
+        // overwritten by a later store), and every load of earlier output
+        // is issued after the stores it reads.
+        if (nx_used) {
+            nx = sg;
+            nx_used = false;
+            sg = load_block(A, blk++, s, n, tail);
+        }
+        if (cst) {
+            uint4 w = cw;
+            if (cst_pat) {
+                // the cpd bytes before the match, repeated with period cpd (the
+                // match that asked for them may be finished and a new one
+                // decoded since: its distance is the request's own, cpd)
+                uint64_t v = ((uint64_t)cw.y << 32) | cw.x;
+                v >>= 8 * (8 - cpd);
+                v &= (1ull << (8 * cpd)) - 1;
+                // (64-bit shifts of 64 or more wrap on the hardware: guard them)
+                if (cpd < 8) v |= v << (8 * cpd);
+                if (cpd < 4) v |= v << (16 * cpd);
+                if (cpd < 2) v |= v << (32 * cpd);
+                if (cpat_st == 1) {   // still the current match
+                    cpat = v;
+                    cpat_st = 2;
+                }
+                w = make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0, 0);
+            }
+            if (csz == 16) *(uint4_u*)(o + cdst) = w;
+            else *(uint2_u*)(o + cdst) = make_uint2(w.x, w.y);
+            cst = false;
+            cst_pat = false;
+        }
+        if (bcnt) {
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j)
+                if (j < bcnt) o[bdst + j] = (uint8_t)(bval >> (8 * j));
+            bcnt = 0;
+        }
+        LP_LAP(9);
+        if (crem) {
+            const uint32_t C = cdist >= 16 ? 16u : 8u;
+            if (cq + C > cap || (cdist < 8 && cq < 8)) {
+                // slot edge: byte by byte, in order (waits; rare)
+                for (uint32_t j = 0; j < crem; ++j) o[cq + j] = (uint8_t)hread1(hs, o, cq + j - cdist);
+                cq += crem;
+                crem = 0;
+            } else if (cdist < 8) {
+                const uint32_t adv0 = 8 - 8 % cdist;
+                const uint32_t adv = adv0 < crem ? adv0 : crem;
+                if (cpat_st == 2) {
+                    *(uint2_u*)(o + cq) = make_uint2((uint32_t)cpat, (uint32_t)(cpat >> 32));
+                    cq += adv;
+                    crem -= adv;
+                } else if (cpat_st == 0) {
+                    const uint64_t v = hread8(hs, o, cq - 8);
+                    cw = make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0, 0);
+                    cst = true;
+                    cst_pat = true;
+                    cpd = cdist;
+                    cdst = cq;
+                    csz = 8;
+                    cpat_st = 1;
+                    cq += adv;
+                    crem -= adv;
+                }
+                // cpat_st == 1 cannot be seen here: the pattern is built in the
+                // memory section that follows the one that requested it
+            } else {
+                if (C == 16) cw = hread16(hs, o, cq - cdist);
+                else {
+                    const uint64_t v = hread8(hs, o, cq - cdist);
+                    cw = make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0, 0);
+                }
+                cst = true;
+                cdst = cq;
+                csz = C;
+                const uint32_t adv = C < crem ? C : crem;
+                cq += adv;
+                crem -= adv;
+            }
+        }
+        LP_LAP(11);
+
+        // ================================================ decode a token
         if (st == S_DATA && crem == 0) {
             refill();
             const int32_t avail = tb + (int32_t)nb;
@@ -275,7 +473,6 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
                 err = ST_INVALID_LITERAL_LENGTH;
             } else if (sym < 256) {
                 drop(L);
-                lit_byte = sym;
             } else if (sym == 256) {
                 drop(L);
                 ev = 1;
@@ -345,10 +542,11 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
                         crem = olen;
                         cdist = dist;
                         cq = pos;
-                        cpat_ok = false;
+                        cpat_st = 0;
                     } else {
-                        emit_lit = true;
-                        lit_pos = pos;
+                        bcnt = 1;
+                        bdst = pos;
+                        bval = sym;
                     }
                     pos += olen;
                 }
@@ -361,16 +559,9 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
                 st = S_DONE;
             }
         }
+        LP_LAP(8);
 
-        // ========================================= B. deferred chunk store
-        if (pend) {
-            if (psz == 16) *(uint4_u*)(o + pdst) = pw;
-            else *(uint2_u*)(o + pdst) = make_uint2(pw.x, pw.y);
-            pend = false;
-        }
-        if (emit_lit) o[lit_pos] = (uint8_t)lit_byte;
-
-        // ======================================= C. block headers, stored
+        // ======================================= block headers, stored
         if (st == S_TYPE) {
             if (last) {
                 result = ST_END_OF_STREAM;
@@ -388,10 +579,20 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
                     if (type == 0) {
                         st = S_SHDR;
                     } else if (type == 1) {
-                        // fixed tables (inflate_stream.ipp:865-930)
+                        // fixed tables (inflate_stream.ipp:865-930): canonical
+                        // order is 256-279 | 0-143 280-287 | 144-255, distances 0-31
                         uint4* dst4 = (uint4*)T;
 #pragma unroll
-                        for (int k = 0; k < 20; ++k) dst4[k] = ((const uint4*)g_fixed_img)[k];
+                        for (int k = 0; k < 20; ++k) {
+                            uint32_t w4[4];
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) {
+                                const int i = 16 * k + 4 * j;
+                                const int v = i < 24 ? i : i < 168 ? i - 24 : i < 176 ? i - 144 : i < 288 ? i - 32 : i - 288;
+                                w4[j] = (uint32_t)v * 0x01010101u + 0x03020100u;
+                            }
+                            dst4[k] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+                        }
                         LE[7] = 0;
                         LE[8] = 168;
                         LE[9] = 288;
@@ -447,13 +648,14 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
             }
         }
         if (st == S_SCOPY) {
+            // COPY (inflate_stream.ipp:206-220): up to 4 bytes per iteration,
+            // stored by the next memory section
             if (srem) {
                 refill();
                 const uint32_t k = srem < 4 ? srem : 4u;
-                const uint32_t w = (uint32_t)bb;
-#pragma unroll
-                for (uint32_t j = 0; j < 4; ++j)
-                    if (j < k) o[pos + j] = (uint8_t)(w >> (8 * j));
+                bval = (uint32_t)bb;
+                bdst = pos;
+                bcnt = k;
                 drop(8 * k);
                 pos += k;
                 srem -= k;
@@ -469,7 +671,6 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
                 }
             }
         }
-
         // ================================================== D. dynamic header
         if (st == S_DYN) {
             // TABLE / LENLENS (inflate_stream.ipp:222-262)
@@ -680,48 +881,9 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
             if (have >= want) st = S_DATA;
         }
 
-        // ======================================================= E. copy step
-        if (crem) {
-            const uint32_t C = cdist >= 16 ? 16u : 8u;
-            if (cq + C > cap || (cdist < 8 && cq < 8)) {
-                // slot edge: byte by byte, in order
-                for (uint32_t j = 0; j < crem; ++j) o[cq + j] = o[cq + j - cdist];
-                cq += crem;
-                crem = 0;
-            } else {
-                uint32_t adv;
-                if (cdist >= 16) {
-                    pw = *(const uint4_u*)(o + cq - cdist);
-                    adv = 16;
-                } else if (cdist >= 8) {
-                    const uint2 v = *(const uint2_u*)(o + cq - cdist);
-                    pw = make_uint4(v.x, v.y, 0, 0);
-                    adv = 8;
-                } else {
-                    if (!cpat_ok) {
-                        // the cdist bytes before cq, repeated (period cdist)
-                        uint64_t v = *(const u64_u*)(o + cq - 8);
-                        v >>= 8 * (8 - cdist);
-                        v &= (1ull << (8 * cdist)) - 1;
-                        // (64-bit shifts of 64 or more wrap on the hardware: guard them)
-                        if (cdist < 8) v |= v << (8 * cdist);
-                        if (cdist < 4) v |= v << (16 * cdist);
-                        if (cdist < 2) v |= v << (32 * cdist);
-                        cpat = v;
-                        cpat_ok = true;
-                    }
-                    pw = make_uint4((uint32_t)cpat, (uint32_t)(cpat >> 32), 0, 0);
-                    adv = 8 - 8 % cdist;
-                }
-                pend = true;
-                pdst = cq;
-                psz = C;
-                if (adv > crem) adv = crem;
-                cq += adv;
-                crem -= adv;
-            }
-        }
+        LP_LAP(10);
     }
+    LP_FLUSH();
     if (valid) {
         out_len[msg] = pos;
         status[msg] = result;
@@ -755,4 +917,19 @@ extern "C" int bpmd_internal_init_fixed_lane(void)
     for (unsigned v = 144; v < 256; ++v) img[k++] = (uint8_t)v;
     for (unsigned v = 0; v < 32; ++v) img[k++] = (uint8_t)v;
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_fixed_img), img, sizeof img);
+}
+
+// diagnostic counters of the lane kernel (meaningful only in the -DBPMD_PROF build)
+extern "C" int bpmd_diag_lane_counters(unsigned long long* out16, int reset)
+{
+    using namespace bpmd::lpm;
+    hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) return (int)e;
+    e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_lprof), sizeof(unsigned long long) * 16);
+    if (e != hipSuccess) return (int)e;
+    if (reset) {
+        unsigned long long z[16] = {0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_lprof), z, sizeof z);
+    }
+    return (int)e;
 }
