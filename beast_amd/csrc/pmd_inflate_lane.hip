@@ -54,30 +54,74 @@ constexpr unsigned STRIDE = 624;   // 64 * 624 = 39 936 B per wave: 4 waves per 
 
 enum : uint32_t { S_TYPE, S_DATA, S_SHDR, S_SCOPY, S_DYN, S_PASS1, S_BUILD, S_PASS2, S_DONE };
 
-struct Tree {
-    uint32_t P[14];   // group of length i + 2: lim << 16 | (i + 2) << 12 | first index
-    uint32_t limend;  // left-justified end of the used code space
-    uint32_t root;    // the reference's (clamped) root table bits
+// Canonical code of up to NB-bit codes, as one word per code length L:
+//   Q[L-1] = lim_L << 15 | L << 11 | end_L
+// lim_L = left-justified end of the codes of length <= L (NB-bit space),
+// end_L = canonical index one past the last code of length L.  The code
+// length of the NB-bit reversed code c is that of the smallest lim_L > c;
+// an unsigned min of Q - ((c + 1) << 15) finds it without compares (words
+// with lim_L <= c wrap to >= 2^31), and a result >= 2^31 means c lies past
+// the used code space (an incomplete or empty code: invalid symbol).
+template <int NB>
+struct Canon {
+    uint32_t Q[NB];
+    uint32_t root;   // the reference's (clamped) root table bits
 };
 
-template <int N>
-__device__ __forceinline__ uint32_t selchain(const uint32_t (&P)[N], uint32_t key)
+template <int NB>
+__device__ __forceinline__ uint32_t canon_min(const uint32_t (&Q)[NB], uint32_t c)
 {
-    uint32_t s = 1u << 12;   // length 1, limit 0, first index 0
+    const uint32_t k1 = (c + 1) << 15;
+    uint32_t m = Q[0] - k1;
 #pragma unroll
-    for (int i = 0; i < N; ++i) s = P[i] <= key ? P[i] : s;
-    return s;
+    for (int i = 1; i + 1 < NB; i += 2) {
+        const uint32_t x = Q[i] - k1, y = Q[i + 1] - k1;
+        m = __builtin_elementwise_min(m, __builtin_elementwise_min(x, y));
+    }
+    if (NB % 2 == 0) m = __builtin_elementwise_min(m, Q[NB - 1] - k1);
+    return m;
+}
+
+struct Sym {
+    uint32_t L;     // code length
+    uint32_t idx;   // canonical index (0 when invalid)
+    bool inval;
+};
+
+template <int NB>
+__device__ __forceinline__ Sym canon_decode(const uint32_t (&Q)[NB], uint32_t c)
+{
+    const uint32_t m = canon_min<NB>(Q, c);
+    Sym r;
+    r.inval = (m >> 31) != 0;
+    const uint32_t q = m + ((c + 1) << 15);
+    r.L = (q >> 11) & 15u;
+    const int32_t below = (int32_t)(c - (q >> 15)) >> (NB - (int32_t)r.L);   // in [-count_L, -1]
+    r.idx = r.inval ? 0u : (uint32_t)((int32_t)(q & 0x7ffu) + below);
+    return r;
+}
+
+// The reference's slow path asks for the root bits, or for root + sub-table
+// index bits when the code is longer than the root: a sub-table covers one
+// root prefix and is as deep as the longest code under it, i.e. the length
+// of the last code of the prefix's range (inflate_stream.ipp:360-420, 688-709).
+template <int NB>
+__device__ __forceinline__ uint32_t canon_need(const Canon<NB>& t, const Sym& y, uint32_t c)
+{
+    if (y.inval || y.L <= t.root) return t.root;
+    const uint32_t re = c | ((1u << (NB - t.root)) - 1u);
+    return ((canon_min<NB>(t.Q, re) + ((re + 1) << 15)) >> 11) & 15u;
 }
 
 __device__ __forceinline__ uint32_t rev15(uint64_t bb) { return __builtin_bitreverse32((uint32_t)bb) >> 17; }
 __device__ __forceinline__ uint32_t lowmask(uint32_t n) { return n >= 32 ? ~0u : ((1u << n) - 1u); }
 
-// counts c[1..15] -> canonical group words; returns 0, 14 or 15 following
+// counts c[1..NB] -> canonical words; returns 0, 14 or 15 following
 // inflate_table's acceptance rules (inflate_stream.ipp:574-617).
 // type: 0 codes, 1 lens, 2 dists.  cum[l] = first canonical index of length l.
 template <int NB>
-__device__ __forceinline__ int make_tree(const uint32_t (&c)[16], uint32_t R, int type, uint32_t (&P)[NB - 1],
-                                         uint32_t& limend, uint32_t& root, uint32_t (&cum)[17])
+__device__ __forceinline__ int make_canon(const uint32_t (&c)[16], uint32_t R, int type, Canon<NB>& t,
+                                          uint32_t (&cum)[17])
 {
     uint32_t hi = 0, lo = 0;
 #pragma unroll
@@ -100,115 +144,86 @@ __device__ __forceinline__ int make_tree(const uint32_t (&c)[16], uint32_t R, in
         cum[l] = cu;
         cu += c[l];
         lim += c[l] << (NB - l);
-        if (l < NB) P[l - 1] = (lim << 16) | ((uint32_t)(l + 1) << 12) | cu;
+        t.Q[l - 1] = (lim << 15) | ((uint32_t)l << 11) | cu;
     }
 #pragma unroll
     for (int l = NB + 1; l <= 16; ++l) cum[l] = cu;
-    limend = lim;
     if (hi == 0) {   // empty code: a 1-bit root of invalid slots
-        root = 1;
+        t.root = 1;
         return 0;
     }
-    uint32_t r = R < hi ? R : hi;
-    root = r < lo ? lo : r;
+    const uint32_t r = R < hi ? R : hi;
+    t.root = r < lo ? lo : r;
     if (over) return ST_OVER_SUBSCRIBED_LENGTH;
     if (left > 0 && (type == 0 || hi != 1)) return ST_INCOMPLETE_LENGTH_SET;
     return 0;
 }
 
-// 16 stream bytes at A + 16*bi: payload bytes [s, s+n) of the lane's
-// message, then the 00 00 FF FF tail (pmd mode), then zeros.  Only blocks
-// wholly inside the payload are read with one 16-byte load; the edges never
-// touch memory outside the payload.
-__device__ __forceinline__ uint4 load_block(const uint8_t* A, uint32_t bi, uint32_t s, uint32_t n, uint32_t tail)
+// Input blocks: 16 stream bytes at A + 16*bi, where the payload is
+// [s, s+n) (A = payload & ~3).  issue_block() reads only dwords holding at
+// least one payload byte -- an aligned dword lies in one page, so nothing
+// past the payload's last page is touched -- and finish_block(), run after
+// the data has arrived, turns the bytes past the payload into the
+// 00 00 FF FF tail (pmd mode) and then zeros.
+__device__ __forceinline__ uint4 issue_block(const uint8_t* A, uint32_t bi, uint32_t s, uint32_t n)
 {
     const uint32_t b0 = bi * 16;
-    if (b0 >= s && b0 + 16 <= s + n) return *(const uint4*)(A + b0);
-    uint32_t w[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const int32_t r = (int32_t)(b0 + j) - (int32_t)s;
-        uint32_t b = 0;
-        if (r >= 0 && (uint32_t)r < n) b = A[b0 + j];
-        else if (r >= 0 && (uint32_t)r - n < tail) b = ((uint32_t)r - n) >= 2 ? 0xffu : 0u;
-        w[j >> 2] |= b << ((j & 3) * 8);
+    if (b0 + 16 <= s + n) return *(const uint4*)(A + b0);
+    const uint32_t* A32 = (const uint32_t*)(A + b0);
+    uint4 w = make_uint4(0, 0, 0, 0);
+    if (b0 + 4 > s && b0 < s + n) w.x = A32[0];
+    if (b0 + 8 > s && b0 + 4 < s + n) w.y = A32[1];
+    if (b0 + 12 > s && b0 + 8 < s + n) w.z = A32[2];
+    if (b0 + 16 > s && b0 + 12 < s + n) w.w = A32[3];
+    return w;
+}
+__device__ __forceinline__ uint32_t finish_dword(uint32_t d, int32_t r0, uint32_t n, uint32_t tail)
+{
+    // r0: payload index of the dword's first byte
+    const int32_t valid = (int32_t)n - r0;
+    if (valid >= 4) return d;
+    d &= valid <= 0 ? 0u : ((1u << (8 * valid)) - 1u);
+    if (tail) {
+        const int32_t t2 = (int32_t)n + 2 - r0, t3 = t2 + 1;   // FF FF of 00 00 FF FF
+        if (t2 >= 0 && t2 < 4) d |= 0xffu << (8 * t2);
+        if (t3 >= 0 && t3 < 4) d |= 0xffu << (8 * t3);
     }
-    return make_uint4(w[0], w[1], w[2], w[3]);
+    return d;
+}
+__device__ __forceinline__ uint4 finish_block(uint4 w, uint32_t bi, uint32_t s, uint32_t n, uint32_t tail)
+{
+    const uint32_t b0 = bi * 16;
+    if (b0 + 16 <= s + n) return w;
+    const int32_t r0 = (int32_t)b0 - (int32_t)s;
+    return make_uint4(finish_dword(w.x, r0, n, tail), finish_dword(w.y, r0 + 4, n, tail),
+                      finish_dword(w.z, r0 + 8, n, tail), finish_dword(w.w, r0 + 12, n, tail));
+}
+
+// In-loop input block bi >= 2 (b0 >= 32): one 16-byte load, clamped to end
+// at E = the end of the payload's last dword (so it never touches a page
+// past the payload), or no load at all past E.  The block's dwords are the
+// loaded ones shifted down by m; finish_in() applies that shift and the tail.
+__device__ __forceinline__ uint32_t in_shift(uint32_t b0, uint32_t E) { return b0 + 16 > E ? (b0 + 16 - E) >> 2 : 0u; }
+__device__ __forceinline__ uint4 finish_in(uint4 w, bool ld, uint32_t bi, uint32_t s, uint32_t n, uint32_t tail)
+{
+    const uint32_t b0 = bi * 16;
+    const uint32_t E = (s + n + 3) & ~3u;
+    if (!ld) w = make_uint4(0, 0, 0, 0);
+    const uint32_t m = ld ? in_shift(b0, E) : 0u;
+    uint4 v = w;
+    if (m == 1) v = make_uint4(w.y, w.z, w.w, 0);
+    if (m == 2) v = make_uint4(w.z, w.w, 0, 0);
+    if (m == 3) v = make_uint4(w.w, 0, 0, 0);
+    return finish_block(v, bi, s, n, tail);
 }
 
 typedef uint4 uint4_u __attribute__((aligned(1)));
 typedef uint2 uint2_u __attribute__((aligned(1)));
 
-// Reads of the lane's own earlier output (match sources).  The vector L1 is
-// not updated by this CU's stores, so a line it cached from an earlier read
-// of the slot could return bytes written since; these reads use the sc1
-// (agent-coherent) policy, which fetches from L2.  Normally one buffer
-// resource based at the wave's lowest slot; if the wave's slots span 4 GiB
-// or more, aligned relaxed agent-scope atomic loads do the same job.
-struct Hist {
-    __amdgpu_buffer_rsrc_t r;
-    uint32_t vb;   // this lane's slot, as an offset from the resource base
-    bool buf;      // wave-uniform
-};
-constexpr int kSc1 = 16;
-
-__device__ __forceinline__ uint64_t aload64(const uint8_t* a)
-{
-    return __hip_atomic_load((const uint64_t*)a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// 8 bytes at o + off (off need not be aligned); every word read lies inside
-// [o + off - 7, o + off + 16)
-__device__ __forceinline__ uint64_t hread8(const Hist& h, const uint8_t* o, uint32_t off)
-{
-    if (h.buf) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b64(h.r, h.vb + off, 0, kSc1);
-        return ((uint64_t)v[1] << 32) | v[0];
-    }
-    const uint8_t* a = o + off;
-    const uint8_t* al = a - ((uintptr_t)a & 7);
-    const unsigned sh = (unsigned)((uintptr_t)a & 7) * 8;
-    const uint64_t lo = aload64(al);
-    if (!sh) return lo;
-    return (lo >> sh) | (aload64(al + 8) << (64 - sh));
-}
-__device__ __forceinline__ uint4 hread16(const Hist& h, const uint8_t* o, uint32_t off)
-{
-    if (h.buf) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(h.r, h.vb + off, 0, kSc1);
-        return make_uint4(v[0], v[1], v[2], v[3]);
-    }
-    const uint64_t a = hread8(h, o, off), b = hread8(h, o, off + 8);
-    return make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
-}
-__device__ __forceinline__ uint32_t hread1(const Hist& h, const uint8_t* o, uint32_t off)
-{
-    if (h.buf) return __builtin_amdgcn_raw_buffer_load_b8(h.r, h.vb + off, 0, kSc1);
-    const uint8_t* a = o + off;
-    const uint32_t* w = (const uint32_t*)(a - ((uintptr_t)a & 3));
-    const uint32_t v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return (v >> (((uintptr_t)a & 3) * 8)) & 0xffu;
-}
-
-__device__ __forceinline__ uint64_t wave_min64(uint64_t x)
-{
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t lo = __shfl_xor((uint32_t)x, d), hi = __shfl_xor((uint32_t)(x >> 32), d);
-        const uint64_t y = ((uint64_t)hi << 32) | lo;
-        x = y < x ? y : x;
-    }
-    return x;
-}
-__device__ __forceinline__ uint64_t wave_max64(uint64_t x)
-{
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t lo = __shfl_xor((uint32_t)x, d), hi = __shfl_xor((uint32_t)(x >> 32), d);
-        const uint64_t y = ((uint64_t)hi << 32) | lo;
-        x = y > x ? y : x;
-    }
-    return x;
-}
+// Reads of the lane's own earlier output (match sources) are plain loads:
+// within one wave the vector L1 is coherent with the wave's own stores
+// (AMDGPU memory model, GFX90A/GFX942: no action is needed for coherence
+// between the lanes of a wavefront).
 
 static __constant__ const uint8_t kClenOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
@@ -253,15 +268,6 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
         cap = out_cap[msg];
         o = out + out_off[msg];
     }
-    Hist hs;
-    {
-        const uint64_t mo = valid ? out_off[msg] : ~0ull;
-        const uint64_t lo = wave_min64(mo);
-        const uint64_t hi = wave_max64(valid ? mo + cap + 64 : 0ull);
-        hs.buf = hi - lo < 0xffffff00ull;
-        hs.r = __builtin_amdgcn_make_buffer_rsrc(out + (hs.buf ? lo : 0), 0, -1, 0x00020000);
-        hs.vb = valid ? (uint32_t)(mo - lo) : 0u;
-    }
     const uint32_t tail = raw ? 0u : 4u;
     const int32_t full_status = raw ? ST_OK : ST_NEED_BUFFERS;
 
@@ -275,29 +281,36 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
     const uint8_t* A = p - s;
     uint4 q = make_uint4(0, 0, 0, 0), nx = q, sg = q;
     if (valid) {
-        q = load_block(A, 0, s, n, tail);
-        nx = load_block(A, 1, s, n, tail);
-        sg = load_block(A, 2, s, n, tail);
+        q = finish_block(issue_block(A, 0, s, n), 0, s, n, tail);
+        nx = finish_block(issue_block(A, 1, s, n), 1, s, n, tail);
     }
-    uint32_t blk = 3, qn = 4;
+    // block 2 goes through the same clamped load and finish_in() as the loop's
+    const uint32_t E_in = (s + n + 3) & ~3u;
+    bool sg_ld = valid && 32 < E_in;
+    if (sg_ld) sg = *(const uint4*)(A + 32 - 4 * in_shift(32, E_in));
+    uint32_t blk = 3, qn = 4, sg_bi = 2;
     bool nx_used = false;   // nx moved into q: refill nx from sg in the next memory section
     uint64_t bb = 0;
     uint32_t nb = 0;
     int32_t tb = (int32_t)(8 * (s + n + tail));   // stream bits not yet moved into bb
+    // branchless: in a wave some lane nearly always needs the refill
     auto refill = [&]() {
-        if (nb <= 32) {
-            bb |= (uint64_t)q.x << nb;
-            nb += 32;
-            tb -= 32;
-            q.x = q.y;
-            q.y = q.z;
-            q.z = q.w;
-            if (--qn == 0) {
-                q = nx;
-                qn = 4;
-                nx_used = true;
-            }
-        }
+        const bool need = nb <= 32;
+        const uint64_t add = (uint64_t)q.x << (nb & 63);
+        bb |= need ? add : 0ull;
+        nb += need ? 32u : 0u;
+        tb -= need ? 32 : 0;
+        q.x = need ? q.y : q.x;
+        q.y = need ? q.z : q.y;
+        q.z = need ? q.w : q.z;
+        qn -= need ? 1u : 0u;
+        const bool sw = qn == 0;
+        q.x = sw ? nx.x : q.x;
+        q.y = sw ? nx.y : q.y;
+        q.z = sw ? nx.z : q.z;
+        q.w = sw ? nx.w : q.w;
+        qn = sw ? 4u : qn;
+        nx_used = nx_used || sw;
     };
     auto drop = [&](uint32_t k) {
         bb >>= k;
@@ -312,18 +325,19 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
     bool last = false;
     uint32_t pos = 0;
 
-    Tree tl, td;
+    Canon<15> tl, td;
 #pragma unroll
-    for (int i = 0; i < 14; ++i) { tl.P[i] = 0; td.P[i] = 0; }
-    tl.limend = td.limend = 0;
+    for (int i = 0; i < 15; ++i) { tl.Q[i] = 0; td.Q[i] = 0; }
     tl.root = 9;
     td.root = 5;
 
     // header state
     uint32_t nlen = 0, ndist = 0, want = 0, have = 0, prev = 0;
     bool eob_seen = false, cl_empty = false;
-    uint32_t PC[6] = {0, 0, 0, 0, 0, 0};
-    uint32_t croot = 1;
+    Canon<7> tc;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) tc.Q[i] = 0;
+    tc.root = 1;
     // stored block
     uint32_t srem = 0;
     bool sfull = false, sstarve = false;
@@ -361,11 +375,11 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
         // Stores go in output order (a chunk's spare tail bytes are always
         // overwritten by a later store), and every load of earlier output
         // is issued after the stores it reads.
-        if (nx_used) {
-            nx = sg;
-            nx_used = false;
-            sg = load_block(A, blk++, s, n, tail);
-        }
+        // consume what the previous memory section loaded (the one wait) ...
+        // (each loaded variable has exactly one load site and is only read
+        // here: a second site would merge into a register copy right after
+        // the load, i.e. an immediate wait)
+        if (nx_used) nx = finish_in(sg, sg_ld, sg_bi, s, n, tail);
         if (cst) {
             uint4 w = cw;
             if (cst_pat) {
@@ -385,23 +399,39 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
                 }
                 w = make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0, 0);
             }
+#ifndef BPMD_EXP_NOSTORE
             if (csz == 16) *(uint4_u*)(o + cdst) = w;
             else *(uint2_u*)(o + cdst) = make_uint2(w.x, w.y);
+#endif
             cst = false;
             cst_pat = false;
         }
         if (bcnt) {
 #pragma unroll
             for (uint32_t j = 0; j < 4; ++j)
+#ifndef BPMD_EXP_NOSTORE
                 if (j < bcnt) o[bdst + j] = (uint8_t)(bval >> (8 * j));
+#else
+                ;
+#endif
             bcnt = 0;
+        }
+        // ... then issue this iteration's loads
+        if (nx_used) {
+            const uint32_t b0 = blk * 16, E = (s + n + 3) & ~3u;
+            sg_ld = b0 < E;
+            if (sg_ld) sg = *(const uint4*)(A + b0 - 4 * in_shift(b0, E));
+            sg_bi = blk++;
+            nx_used = false;
         }
         LP_LAP(9);
         if (crem) {
             const uint32_t C = cdist >= 16 ? 16u : 8u;
+            bool ld = false;
+            uint32_t src = 0;
             if (cq + C > cap || (cdist < 8 && cq < 8)) {
                 // slot edge: byte by byte, in order (waits; rare)
-                for (uint32_t j = 0; j < crem; ++j) o[cq + j] = (uint8_t)hread1(hs, o, cq + j - cdist);
+                for (uint32_t j = 0; j < crem; ++j) o[cq + j] = o[cq + j - cdist];
                 cq += crem;
                 crem = 0;
             } else if (cdist < 8) {
@@ -412,31 +442,31 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
                     cq += adv;
                     crem -= adv;
                 } else if (cpat_st == 0) {
-                    const uint64_t v = hread8(hs, o, cq - 8);
-                    cw = make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0, 0);
-                    cst = true;
+                    ld = true;
+                    src = cq - 8;
                     cst_pat = true;
                     cpd = cdist;
-                    cdst = cq;
                     csz = 8;
                     cpat_st = 1;
+                    cdst = cq;
                     cq += adv;
                     crem -= adv;
                 }
                 // cpat_st == 1 cannot be seen here: the pattern is built in the
                 // memory section that follows the one that requested it
             } else {
-                if (C == 16) cw = hread16(hs, o, cq - cdist);
-                else {
-                    const uint64_t v = hread8(hs, o, cq - cdist);
-                    cw = make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0, 0);
-                }
-                cst = true;
-                cdst = cq;
+                ld = true;
+                src = cq - cdist;
                 csz = C;
+                cdst = cq;
                 const uint32_t adv = C < crem ? C : crem;
                 cq += adv;
                 crem -= adv;
+            }
+            if (ld) {
+                // 16 bytes from src: never past cq + 8 <= cap (C = 8 cases) or cq
+                cw = *(const uint4_u*)(o + src);
+                cst = true;
             }
         }
         LP_LAP(11);
@@ -446,23 +476,35 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
             refill();
             const int32_t avail = tb + (int32_t)nb;
             const uint32_t c15 = rev15(bb);
-            const uint32_t sel = selchain(tl.P, (c15 << 16) | 0xffffu);
-            const uint32_t L = (sel >> 12) & 15u;
-            bool inval = c15 >= tl.limend;
-            uint32_t idx = (sel & 0xfffu) + ((c15 - (sel >> 16)) >> (15u - L));
-            idx = inval ? 0u : idx;
+            const Sym y = canon_decode<15>(tl.Q, c15);
+            const uint32_t L = y.L;
+            bool inval = y.inval;
+            const uint32_t idx = y.idx;
             const uint32_t le = LE[L];
             uint32_t sym = T[O_LIT + idx] + (idx >= le ? 256u : 0u);
             inval |= sym >= 286;
             uint32_t need_l = 0;
-            if (avail < 48) {
-                need_l = tl.root;
-                if (!inval && L > tl.root) {
-                    const uint32_t re = c15 | lowmask(15u - tl.root);
-                    need_l = (selchain(tl.P, (re << 16) | 0xffffu) >> 12) & 15u;
-                }
-            }
-            uint32_t len = 0, dist = 0;
+            if (avail < 48) need_l = canon_need<15>(tl, y, c15);
+            // length and distance are decoded for every lane (a wave nearly
+            // always holds a match): no divergent branch around them
+            const bool is_len = !inval && sym > 256;
+            const uint32_t li = is_len ? sym - 257 : 0u;
+            const uint32_t xl = (li < 8 || li == 28) ? 0u : ((li - 4) >> 2);
+            uint32_t len = li < 8 ? li + 3 : (li == 28 ? 258u : (((4u + (li & 3)) << xl) + 3));
+            len += (uint32_t)(bb >> L) & lowmask(xl);
+            const uint32_t used = L + (is_len ? xl : 0u);
+            drop(used);
+            refill();
+            const uint32_t d15 = rev15(bb);
+            const Sym yd = canon_decode<15>(td.Q, d15);
+            const uint32_t Ld = yd.L;
+            const uint32_t dsym = T[O_DST + yd.idx];
+            const bool invd = yd.inval || dsym >= 30;
+            const uint32_t xd = dsym < 4 ? 0u : (dsym >> 1) - 1;
+            uint32_t dist = dsym < 4 ? dsym + 1 : (((2u + (dsym & 1)) << xd) + 1);
+            dist += (uint32_t)(bb >> Ld) & lowmask(xd);
+            uint32_t need_d = 0;
+            if (avail < 48 && is_len) need_d = canon_need<15>(td, yd, d15);
             bool is_match = false;
             uint32_t ev = 0;   // 0 token, 1 eob, 2 starved, 3 error
             int32_t err = 0;
@@ -471,53 +513,19 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
             } else if (inval) {
                 ev = 3;
                 err = ST_INVALID_LITERAL_LENGTH;
-            } else if (sym < 256) {
-                drop(L);
             } else if (sym == 256) {
-                drop(L);
                 ev = 1;
-            } else {
-                const uint32_t li = sym - 257;
-                const uint32_t xl = (li < 8 || li == 28) ? 0u : ((li - 4) >> 2);
-                len = li < 8 ? li + 3 : (li == 28 ? 258u : (((4u + (li & 3)) << xl) + 3));
-                len += (uint32_t)(bb >> L) & lowmask(xl);
-                const uint32_t used = L + xl;
-                if ((int32_t)used > avail) {
+            } else if (sym > 256) {
+                if ((int32_t)used > avail || (int32_t)(used + need_d) > avail) {
+                    ev = 2;
+                } else if (invd) {
+                    ev = 3;
+                    err = ST_INVALID_DISTANCE_CODE;
+                } else if ((int32_t)(used + Ld + xd) > avail) {
                     ev = 2;
                 } else {
-                    drop(used);
-                    refill();
-                    const uint32_t d15 = rev15(bb);
-                    const uint32_t seld = selchain(td.P, (d15 << 16) | 0xffffu);
-                    const uint32_t Ld = (seld >> 12) & 15u;
-                    bool invd = d15 >= td.limend;
-                    uint32_t idd = (seld & 0xfffu) + ((d15 - (seld >> 16)) >> (15u - Ld));
-                    idd = invd ? 0u : idd;
-                    const uint32_t dsym = T[O_DST + idd];
-                    invd |= dsym >= 30;
-                    uint32_t need_d = 0;
-                    if (avail < 48) {
-                        need_d = td.root;
-                        if (!invd && Ld > td.root) {
-                            const uint32_t re = d15 | lowmask(15u - td.root);
-                            need_d = (selchain(td.P, (re << 16) | 0xffffu) >> 12) & 15u;
-                        }
-                    }
-                    if ((int32_t)(used + need_d) > avail) {
-                        ev = 2;
-                    } else if (invd) {
-                        ev = 3;
-                        err = ST_INVALID_DISTANCE_CODE;
-                    } else {
-                        const uint32_t xd = dsym < 4 ? 0u : (dsym >> 1) - 1;
-                        dist = dsym < 4 ? dsym + 1 : (((2u + (dsym & 1)) << xd) + 1);
-                        dist += (uint32_t)(bb >> Ld) & lowmask(xd);
-                        if ((int32_t)(used + Ld + xd) > avail) ev = 2;
-                        else {
-                            drop(Ld + xd);
-                            is_match = true;
-                        }
-                    }
+                    drop(Ld + xd);
+                    is_match = true;
                 }
             }
             if (ev == 0) {
@@ -602,11 +610,11 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
                         c[7] = 24;
                         c[8] = 152;
                         c[9] = 112;
-                        make_tree<15>(c, 9, 1, tl.P, tl.limend, tl.root, cum);
+                        make_canon<15>(c, 9, 1, tl, cum);
 #pragma unroll
                         for (int l = 0; l < 16; ++l) c[l] = 0;
                         c[5] = 32;
-                        make_tree<15>(c, 5, 2, td.P, td.limend, td.root, cum);
+                        make_canon<15>(c, 5, 2, td, cum);
                         st = S_DATA;
                     } else if (type == 2) {
                         st = S_DYN;
@@ -708,9 +716,7 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
                     uint32_t c[16], cum[17];
 #pragma unroll
                     for (int l = 0; l < 16; ++l) c[l] = (l >= 1 && l <= 7) ? (uint32_t)(acc >> (5 * l)) & 31u : 0u;
-                    uint32_t limend_c;
-                    const int e = make_tree<7>(c, 7, 0, PC, limend_c, croot, cum);
-                    (void)limend_c;
+                    const int e = make_canon<7>(c, 7, 0, tc, cum);
                     cl_empty = c[1] + c[2] + c[3] + c[4] + c[5] + c[6] + c[7] == 0;
                     if (e) {
                         result = e;
@@ -748,12 +754,11 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
             uint32_t L = 1, csym = 0;
             if (!cl_empty) {
                 const uint32_t c7 = __builtin_bitreverse32((uint32_t)bb) >> 25;
-                const uint32_t sel = selchain(PC, (c7 << 16) | 0xffffu);
-                L = (sel >> 12) & 15u;
-                const uint32_t idx = (sel & 0xfffu) + ((c7 - (sel >> 16)) >> (7u - L));
-                csym = T[O_CLS + (idx < 19 ? idx : 0u)];
+                const Sym yc = canon_decode<7>(tc.Q, c7);
+                L = yc.L;
+                csym = T[O_CLS + (yc.idx < 19 ? yc.idx : 0u)];
             }
-            if (avail < (int32_t)croot) {
+            if (avail < (int32_t)tc.root) {
                 st = S_DONE;
             } else {
                 uint32_t val = csym, rep = 1, used = L;
@@ -831,11 +836,11 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
                 c[0] = 0;
 #pragma unroll
                 for (int l = 1; l < 16; ++l) c[l] = h[l] & 0x3ffu;
-                int e = make_tree<15>(c, 9, 1, tl.P, tl.limend, tl.root, cuml);
+                int e = make_canon<15>(c, 9, 1, tl, cuml);
                 if (!e) {
 #pragma unroll
                     for (int l = 1; l < 16; ++l) c[l] = (h[l] >> 20) & 0x3ffu;
-                    e = make_tree<15>(c, 6, 2, td.P, td.limend, td.root, cumd);
+                    e = make_canon<15>(c, 6, 2, td, cumd);
                 }
                 if (e) {
                     result = e;
