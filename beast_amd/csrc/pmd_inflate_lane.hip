@@ -52,6 +52,14 @@ constexpr unsigned O_CLS = 416;    // u8[20]   code-length code symbols, canonic
 constexpr unsigned O_NIB = 448;    // u8[160]  code lengths, one nibble per symbol
 constexpr unsigned STRIDE = 624;   // 64 * 624 = 39 936 B per wave: 4 waves per CU
 
+#ifndef BPMD_KLIT
+#define BPMD_KLIT 4
+#endif
+constexpr int KLIT = BPMD_KLIT;   // symbols decoded per iteration when literals lead
+static_assert(KLIT >= 1 && KLIT <= 4, "literal bytes are queued in one 32-bit word");
+constexpr int KCL = 4;            // code-length symbols per iteration (pass 1)
+constexpr int KNIB = 16;          // code lengths placed per iteration (pass 2)
+
 enum : uint32_t { S_TYPE, S_DATA, S_SHDR, S_SCOPY, S_DYN, S_PASS1, S_BUILD, S_PASS2, S_DONE };
 
 // Canonical code of up to NB-bit codes, as one word per code length L:
@@ -225,6 +233,23 @@ typedef uint2 uint2_u __attribute__((aligned(1)));
 // (AMDGPU memory model, GFX90A/GFX942: no action is needed for coherence
 // between the lanes of a wavefront).
 
+// Store the first n of the sz (8 or 16) bytes of w at o + dst, never past
+// o + lim: whole when it fits (spare bytes past n are overwritten by later
+// output), byte by byte from registers at the end of the slot.
+__device__ __forceinline__ void store_bounded(uint8_t* o, uint32_t dst, uint32_t sz, uint32_t lim, uint4 w)
+{
+    if (dst + sz <= lim) {
+        if (sz == 16) *(uint4_u*)(o + dst) = w;
+        else *(uint2_u*)(o + dst) = make_uint2(w.x, w.y);
+        return;
+    }
+    const uint32_t k = lim - dst;   // < sz
+    const uint32_t d[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j)
+        if (j < k) o[dst + j] = (uint8_t)(d[j >> 2] >> (8 * (j & 3)));
+}
+
 static __constant__ const uint8_t kClenOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
 // fixed-code canonical symbol image (low 8 bits): lengths 7: 256-279,
@@ -347,7 +372,7 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
     uint32_t cpat_st = 0;   // dist < 8: 0 pattern not requested, 1 source bytes in flight, 2 pattern ready
     // chunk loaded in the previous memory section, stored in the next one
     bool cst = false, cst_pat = false;
-    uint32_t cdst = 0, csz = 0, cpd = 1;
+    uint32_t cdst = 0, csz = 0, cpd = 1, csh = 0;
     uint4 cw = make_uint4(0, 0, 0, 0);
     // byte stores decided by the previous compute section (literal or stored-block bytes)
     uint32_t bcnt = 0, bdst = 0, bval = 0;
@@ -387,7 +412,7 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
                 // match that asked for them may be finished and a new one
                 // decoded since: its distance is the request's own, cpd)
                 uint64_t v = ((uint64_t)cw.y << 32) | cw.x;
-                v >>= 8 * (8 - cpd);
+                v >>= 8 * csh;
                 v &= (1ull << (8 * cpd)) - 1;
                 // (64-bit shifts of 64 or more wrap on the hardware: guard them)
                 if (cpd < 8) v |= v << (8 * cpd);
@@ -400,8 +425,7 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
                 w = make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0, 0);
             }
 #ifndef BPMD_EXP_NOSTORE
-            if (csz == 16) *(uint4_u*)(o + cdst) = w;
-            else *(uint2_u*)(o + cdst) = make_uint2(w.x, w.y);
+            store_bounded(o, cdst, csz, cap, w);
 #endif
             cst = false;
             cst_pat = false;
@@ -429,21 +453,19 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
             const uint32_t C = cdist >= 16 ? 16u : 8u;
             bool ld = false;
             uint32_t src = 0;
-            if (cq + C > cap || (cdist < 8 && cq < 8)) {
-                // slot edge: byte by byte, in order (waits; rare)
-                for (uint32_t j = 0; j < crem; ++j) o[cq + j] = o[cq + j - cdist];
-                cq += crem;
-                crem = 0;
-            } else if (cdist < 8) {
+            if (cdist < 8) {
                 const uint32_t adv0 = 8 - 8 % cdist;
                 const uint32_t adv = adv0 < crem ? adv0 : crem;
                 if (cpat_st == 2) {
-                    *(uint2_u*)(o + cq) = make_uint2((uint32_t)cpat, (uint32_t)(cpat >> 32));
+                    store_bounded(o, cq, 8, cap, make_uint4((uint32_t)cpat, (uint32_t)(cpat >> 32), 0, 0));
                     cq += adv;
                     crem -= adv;
                 } else if (cpat_st == 0) {
+                    // the cdist bytes before cq, read as 8 bytes that never
+                    // start before the slot
                     ld = true;
-                    src = cq - 8;
+                    src = cq >= 8 ? cq - 8 : 0u;
+                    csh = cq - cdist - src;
                     cst_pat = true;
                     cpd = cdist;
                     csz = 8;
@@ -464,113 +486,155 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
                 crem -= adv;
             }
             if (ld) {
-                // 16 bytes from src: never past cq + 8 <= cap (C = 8 cases) or cq
+                // 16 bytes from src: the bytes used all lie in [src, cq); the
+                // rest of the 16 may run into the next slot (never stored)
                 cw = *(const uint4_u*)(o + src);
                 cst = true;
             }
         }
         LP_LAP(11);
 
+        // Input bits per iteration stay <= 108 (the reader always holds >= 160
+        // without touching memory): a state entered during an iteration runs
+        // from the next one, except that a block header may run in the same
+        // iteration as its type bits (<= 74 bits together).
+        const uint32_t st0 = st;
         // ================================================ decode a token
         if (st == S_DATA && crem == 0) {
+            // Up to KLIT symbols per iteration: while there is room for them
+            // (input for KLIT - 1 literals plus a whole token, output for
+            // KLIT literals, so no event can occur among them) leading
+            // literals are taken directly; the first other symbol -- or, out
+            // of room, the first symbol of any kind -- is the iteration's main
+            // token, handled with the reference's checks below.  (Deflated
+            // text: 65 % of tokens are literals, in runs of ~3.7.)
             refill();
-            const int32_t avail = tb + (int32_t)nb;
-            const uint32_t c15 = rev15(bb);
-            const Sym y = canon_decode<15>(tl.Q, c15);
-            const uint32_t L = y.L;
-            bool inval = y.inval;
-            const uint32_t idx = y.idx;
-            const uint32_t le = LE[L];
-            uint32_t sym = T[O_LIT + idx] + (idx >= le ? 256u : 0u);
-            inval |= sym >= 286;
-            uint32_t need_l = 0;
-            if (avail < 48) need_l = canon_need<15>(tl, y, c15);
-            // length and distance are decoded for every lane (a wave nearly
-            // always holds a match): no divergent branch around them
-            const bool is_len = !inval && sym > 256;
-            const uint32_t li = is_len ? sym - 257 : 0u;
-            const uint32_t xl = (li < 8 || li == 28) ? 0u : ((li - 4) >> 2);
-            uint32_t len = li < 8 ? li + 3 : (li == 28 ? 258u : (((4u + (li & 3)) << xl) + 3));
-            len += (uint32_t)(bb >> L) & lowmask(xl);
-            const uint32_t used = L + (is_len ? xl : 0u);
-            drop(used);
-            refill();
-            const uint32_t d15 = rev15(bb);
-            const Sym yd = canon_decode<15>(td.Q, d15);
-            const uint32_t Ld = yd.L;
-            const uint32_t dsym = T[O_DST + yd.idx];
-            const bool invd = yd.inval || dsym >= 30;
-            const uint32_t xd = dsym < 4 ? 0u : (dsym >> 1) - 1;
-            uint32_t dist = dsym < 4 ? dsym + 1 : (((2u + (dsym & 1)) << xd) + 1);
-            dist += (uint32_t)(bb >> Ld) & lowmask(xd);
-            uint32_t need_d = 0;
-            if (avail < 48 && is_len) need_d = canon_need<15>(td, yd, d15);
-            bool is_match = false;
-            uint32_t ev = 0;   // 0 token, 1 eob, 2 starved, 3 error
-            int32_t err = 0;
-            if ((int32_t)need_l > avail) {
-                ev = 2;
-            } else if (inval) {
-                ev = 3;
-                err = ST_INVALID_LITERAL_LENGTH;
-            } else if (sym == 256) {
-                ev = 1;
-            } else if (sym > 256) {
-                if ((int32_t)used > avail || (int32_t)(used + need_d) > avail) {
-                    ev = 2;
-                } else if (invd) {
-                    ev = 3;
-                    err = ST_INVALID_DISTANCE_CODE;
-                } else if ((int32_t)(used + Ld + xd) > avail) {
-                    ev = 2;
-                } else {
-                    drop(Ld + xd);
-                    is_match = true;
+            const bool multi = (tb + (int32_t)nb) >= 48 + 15 * (KLIT - 1) && pos + KLIT <= cap;
+            bool found = false;
+            uint32_t nlit = 0, lbytes = 0;
+            int32_t avail = 0;
+            uint32_t c15 = 0, L = 0, sym = 0;
+            Sym y;
+            bool inval = false;
+#pragma unroll
+            for (int k = 0; k < KLIT; ++k) {
+                if (k > 0) refill();   // appends above the unconsumed bits only: harmless for finished lanes
+                const bool act = !found && (k == 0 || multi);
+                const uint32_t kc = rev15(bb);
+                const Sym ky = canon_decode<15>(tl.Q, kc);
+                const uint32_t kle = LE[ky.L];
+                const uint32_t ks = T[O_LIT + ky.idx] + (ky.idx >= kle ? 256u : 0u);
+                const bool kinv = ky.inval || ks >= 286;
+                if (act && multi && !kinv && ks < 256) {
+                    drop(ky.L);
+                    lbytes |= ks << (8 * nlit);
+                    ++nlit;
+                } else if (act) {
+                    found = true;
+                    avail = tb + (int32_t)nb;
+                    c15 = kc;
+                    y = ky;
+                    L = ky.L;
+                    sym = ks;
+                    inval = kinv;
                 }
             }
-            if (ev == 0) {
-                // output checks in the reference's order (inflate_stream.ipp:475-514)
-                if (raw && pos >= cap) {
-                    result = full_status;
-                    st = S_DONE;
-                } else if (is_match && dist > pos) {
-                    result = ST_INVALID_DISTANCE;
-                    st = S_DONE;
-                } else if (pos >= cap) {
-                    result = full_status;
-                    st = S_DONE;
-                } else {
-                    uint32_t olen = is_match ? len : 1u;
-                    if (pos + olen > cap) {
-                        olen = cap - pos;
+            if (nlit) {
+                bcnt = nlit;
+                bdst = pos;
+                bval = lbytes;
+                pos += nlit;
+            }
+            if (found) {
+                uint32_t need_l = 0;
+                if (avail < 48) need_l = canon_need<15>(tl, y, c15);
+                // length and distance are decoded for every lane (a wave nearly
+                // always holds a match): no divergent branch around them
+                const bool is_len = !inval && sym > 256;
+                const uint32_t li = is_len ? sym - 257 : 0u;
+                const uint32_t xl = (li < 8 || li == 28) ? 0u : ((li - 4) >> 2);
+                uint32_t len = li < 8 ? li + 3 : (li == 28 ? 258u : (((4u + (li & 3)) << xl) + 3));
+                len += (uint32_t)(bb >> L) & lowmask(xl);
+                const uint32_t used = L + (is_len ? xl : 0u);
+                drop(used);
+                refill();
+                const uint32_t d15 = rev15(bb);
+                const Sym yd = canon_decode<15>(td.Q, d15);
+                const uint32_t Ld = yd.L;
+                const uint32_t dsym = T[O_DST + yd.idx];
+                const bool invd = yd.inval || dsym >= 30;
+                const uint32_t xd = dsym < 4 ? 0u : (dsym >> 1) - 1;
+                uint32_t dist = dsym < 4 ? dsym + 1 : (((2u + (dsym & 1)) << xd) + 1);
+                dist += (uint32_t)(bb >> Ld) & lowmask(xd);
+                uint32_t need_d = 0;
+                if (avail < 48 && is_len) need_d = canon_need<15>(td, yd, d15);
+                bool is_match = false;
+                uint32_t ev = 0;   // 0 token, 1 eob, 2 starved, 3 error
+                int32_t err = 0;
+                if ((int32_t)need_l > avail) {
+                    ev = 2;
+                } else if (inval) {
+                    ev = 3;
+                    err = ST_INVALID_LITERAL_LENGTH;
+                } else if (sym == 256) {
+                    ev = 1;
+                } else if (sym > 256) {
+                    if ((int32_t)used > avail || (int32_t)(used + need_d) > avail) {
+                        ev = 2;
+                    } else if (invd) {
+                        ev = 3;
+                        err = ST_INVALID_DISTANCE_CODE;
+                    } else if ((int32_t)(used + Ld + xd) > avail) {
+                        ev = 2;
+                    } else {
+                        drop(Ld + xd);
+                        is_match = true;
+                    }
+                }
+                if (ev == 0) {
+                    // output checks in the reference's order (inflate_stream.ipp:475-514)
+                    if (raw && pos >= cap) {
                         result = full_status;
                         st = S_DONE;
-                    }
-                    if (is_match) {
-                        crem = olen;
-                        cdist = dist;
-                        cq = pos;
-                        cpat_st = 0;
+                    } else if (is_match && dist > pos) {
+                        result = ST_INVALID_DISTANCE;
+                        st = S_DONE;
+                    } else if (pos >= cap) {
+                        result = full_status;
+                        st = S_DONE;
                     } else {
-                        bcnt = 1;
-                        bdst = pos;
-                        bval = sym;
+                        uint32_t olen = is_match ? len : 1u;
+                        if (pos + olen > cap) {
+                            olen = cap - pos;
+                            result = full_status;
+                            st = S_DONE;
+                        }
+                        if (is_match) {
+                            crem = olen;
+                            cdist = dist;
+                            cq = pos;
+                            cpat_st = 0;
+                        } else {
+                            bcnt = 1;
+                            bdst = pos;
+                            bval = sym;
+                        }
+                        pos += olen;
                     }
-                    pos += olen;
+                } else if (ev == 1) {
+                    st = S_TYPE;
+                } else if (ev == 2) {
+                    st = S_DONE;
+                } else {
+                    result = err;
+                    st = S_DONE;
                 }
-            } else if (ev == 1) {
-                st = S_TYPE;
-            } else if (ev == 2) {
-                st = S_DONE;
-            } else {
-                result = err;
-                st = S_DONE;
             }
         }
         LP_LAP(8);
 
         // ======================================= block headers, stored
-        if (st == S_TYPE) {
+        if (st == S_TYPE && st0 == S_TYPE) {
             if (last) {
                 result = ST_END_OF_STREAM;
                 st = S_DONE;
@@ -657,8 +721,9 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
         }
         if (st == S_SCOPY) {
             // COPY (inflate_stream.ipp:206-220): up to 4 bytes per iteration,
-            // stored by the next memory section
-            if (srem) {
+            // stored by the next memory section (after any literals this
+            // iteration already queued before its end of block)
+            if (srem && bcnt == 0) {
                 refill();
                 const uint32_t k = srem < 4 ? srem : 4u;
                 bval = (uint32_t)bb;
@@ -668,7 +733,7 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
                 pos += k;
                 srem -= k;
             }
-            if (srem == 0) {
+            if (srem == 0 && bcnt == 0) {
                 if (sfull) {
                     result = full_status;
                     st = S_DONE;
@@ -747,75 +812,77 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
                 }
             }
         }
-        if (st == S_PASS1) {
-            // CODELENS (inflate_stream.ipp:264-327), one symbol per iteration
-            refill();
-            const int32_t avail = tb + (int32_t)nb;
-            uint32_t L = 1, csym = 0;
-            if (!cl_empty) {
-                const uint32_t c7 = __builtin_bitreverse32((uint32_t)bb) >> 25;
-                const Sym yc = canon_decode<7>(tc.Q, c7);
-                L = yc.L;
-                csym = T[O_CLS + (yc.idx < 19 ? yc.idx : 0u)];
-            }
-            if (avail < (int32_t)tc.root) {
-                st = S_DONE;
-            } else {
-                uint32_t val = csym, rep = 1, used = L;
-                bool ok = true;
-                if (csym >= 16) {
-                    const uint32_t xb = csym == 16 ? 2u : (csym == 17 ? 3u : 7u);
-                    if (avail < (int32_t)(L + xb)) {
-                        st = S_DONE;
-                        ok = false;
-                    } else {
-                        const uint32_t x = (uint32_t)(bb >> L) & lowmask(xb);
-                        used = L + xb;
-                        if (csym == 16) {
-                            if (have == 0) {
+#pragma unroll
+        for (int kc = 0; kc < KCL; ++kc) {
+            if (st != S_PASS1 || st0 != S_PASS1) break;
+                // CODELENS (inflate_stream.ipp:264-327), up to KCL symbols per iteration
+                refill();
+                const int32_t avail = tb + (int32_t)nb;
+                uint32_t L = 1, csym = 0;
+                if (!cl_empty) {
+                    const uint32_t c7 = __builtin_bitreverse32((uint32_t)bb) >> 25;
+                    const Sym yc = canon_decode<7>(tc.Q, c7);
+                    L = yc.L;
+                    csym = T[O_CLS + (yc.idx < 19 ? yc.idx : 0u)];
+                }
+                if (avail < (int32_t)tc.root) {
+                    st = S_DONE;
+                } else {
+                    uint32_t val = csym, rep = 1, used = L;
+                    bool ok = true;
+                    if (csym >= 16) {
+                        const uint32_t xb = csym == 16 ? 2u : (csym == 17 ? 3u : 7u);
+                        if (avail < (int32_t)(L + xb)) {
+                            st = S_DONE;
+                            ok = false;
+                        } else {
+                            const uint32_t x = (uint32_t)(bb >> L) & lowmask(xb);
+                            used = L + xb;
+                            if (csym == 16) {
+                                if (have == 0) {
+                                    result = ST_INVALID_BIT_LENGTH_REPEAT;
+                                    st = S_DONE;
+                                    ok = false;
+                                }
+                                val = prev;
+                                rep = 3 + x;
+                            } else {
+                                val = 0;
+                                rep = (csym == 17 ? 3u : 11u) + x;
+                            }
+                            if (ok && have + rep > want) {
                                 result = ST_INVALID_BIT_LENGTH_REPEAT;
                                 st = S_DONE;
                                 ok = false;
                             }
-                            val = prev;
-                            rep = 3 + x;
-                        } else {
-                            val = 0;
-                            rep = (csym == 17 ? 3u : 11u) + x;
-                        }
-                        if (ok && have + rep > want) {
-                            result = ST_INVALID_BIT_LENGTH_REPEAT;
-                            st = S_DONE;
-                            ok = false;
                         }
                     }
-                }
-                if (ok) {
-                    drop(used);
-                    if (val) {
-                        const uint32_t a = have, b = have + rep;
-                        const uint64_t pat = ((uint64_t)val * 0x1111111111111111ull) & ((1ull << (4 * rep)) - 1);
-                        const uint64_t v = pat << ((a & 7) * 4);
-                        uint32_t* nw = (uint32_t*)(T + O_NIB) + (a >> 3);
-                        __hip_atomic_fetch_or(nw, (uint32_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        if ((uint32_t)(v >> 32))
-                            __hip_atomic_fetch_or(nw + 1, (uint32_t)(v >> 32), __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
-                        const uint32_t e_l = b < nlen ? b : nlen;
-                        const uint32_t nl = e_l > a ? e_l - a : 0u;
-                        const uint32_t e_o = b < 256 ? b : 256u;
-                        const uint32_t nlo = e_o > a ? e_o - a : 0u;
-                        const uint32_t s_d = a > nlen ? a : nlen;
-                        const uint32_t nd = b > s_d ? b - s_d : 0u;
-                        __hip_atomic_fetch_add(H + val, nl | (nlo << 10) | (nd << 20), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP);
-                        if (a <= 256 && 256 < b) eob_seen = true;
+                    if (ok) {
+                        drop(used);
+                        if (val) {
+                            const uint32_t a = have, b = have + rep;
+                            const uint64_t pat = ((uint64_t)val * 0x1111111111111111ull) & ((1ull << (4 * rep)) - 1);
+                            const uint64_t v = pat << ((a & 7) * 4);
+                            uint32_t* nw = (uint32_t*)(T + O_NIB) + (a >> 3);
+                            __hip_atomic_fetch_or(nw, (uint32_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            if ((uint32_t)(v >> 32))
+                                __hip_atomic_fetch_or(nw + 1, (uint32_t)(v >> 32), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+                            const uint32_t e_l = b < nlen ? b : nlen;
+                            const uint32_t nl = e_l > a ? e_l - a : 0u;
+                            const uint32_t e_o = b < 256 ? b : 256u;
+                            const uint32_t nlo = e_o > a ? e_o - a : 0u;
+                            const uint32_t s_d = a > nlen ? a : nlen;
+                            const uint32_t nd = b > s_d ? b - s_d : 0u;
+                            __hip_atomic_fetch_add(H + val, nl | (nlo << 10) | (nd << 20), __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+                            if (a <= 256 && 256 < b) eob_seen = true;
+                        }
+                        prev = val;
+                        have += rep;
+                        if (have == want) st = S_BUILD;
                     }
-                    prev = val;
-                    have += rep;
-                    if (have == want) st = S_BUILD;
                 }
-            }
         }
         if (st == S_BUILD) {
             if (!eob_seen) {
@@ -868,21 +935,30 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
         }
         if (st == S_PASS2) {
             // place symbols in canonical order (inflate_stream.ipp:632-640)
-            const uint32_t w = ((const uint32_t*)(T + O_NIB))[have >> 3];
 #pragma unroll
-            for (uint32_t k = 0; k < 8; ++k) {
-                const uint32_t i = have + k;
-                const uint32_t l = (w >> (4 * k)) & 15u;
-                const bool isl = i < nlen;
-                const uint32_t inc = (l && i < want) ? (isl ? 1u : 0x10000u) : 0u;
-                if (inc) {
-                    const uint32_t old = __hip_atomic_fetch_add(H + l, inc, __ATOMIC_RELAXED,
-                                                                __HIP_MEMORY_SCOPE_WORKGROUP);
-                    if (isl) T[O_LIT + (old & 0xffffu)] = (uint8_t)i;
-                    else T[O_DST + (old >> 16)] = (uint8_t)(i - nlen);
+            for (uint32_t h8 = 0; h8 < KNIB; h8 += 8) {
+                const uint32_t w = ((const uint32_t*)(T + O_NIB))[(have + h8) >> 3];
+                uint32_t olds[8];
+                // all fetch-adds first (no branch between them), then the
+                // placements: one LDS round trip for the eight
+#pragma unroll
+                for (uint32_t k = 0; k < 8; ++k) {
+                    const uint32_t i = have + h8 + k;
+                    const uint32_t l = (w >> (4 * k)) & 15u;
+                    const uint32_t inc = (l && i < want) ? (i < nlen ? 1u : 0x10000u) : 0u;
+                    olds[k] = __hip_atomic_fetch_add(H + l, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+#pragma unroll
+                for (uint32_t k = 0; k < 8; ++k) {
+                    const uint32_t i = have + h8 + k;
+                    const uint32_t l = (w >> (4 * k)) & 15u;
+                    if (l && i < want) {
+                        if (i < nlen) T[O_LIT + (olds[k] & 0xffffu)] = (uint8_t)i;
+                        else T[O_DST + (olds[k] >> 16)] = (uint8_t)(i - nlen);
+                    }
                 }
             }
-            have += 8;
+            have += KNIB;
             if (have >= want) st = S_DATA;
         }
 

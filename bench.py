@@ -135,7 +135,7 @@ def pmc_traffic(kernel):
         fetch, write = [], []
         with open(f) as fh:
             for r in csv.DictReader(fh):
-                if kernel not in r["kernel"]:
+                if r["kernel"].split("::")[-1] != kernel:
                     continue
                 (fetch if r["counter"] == "FETCH_SIZE" else write).append(float(r["value_kB"]))
         if fetch and write:
@@ -228,7 +228,8 @@ def main():
     value = uncomp * world / (1 << 30) / step_s
     alg_bytes = comp + uncomp + 16 * n
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic("inflate_kernel") if n == N_MSGS else (None, None)
+    kname = "inflate_lane_kernel" if n >= 2048 else "inflate_kernel"   # bpmd_set_inflate_kernel(0) policy
+    traffic, traffic_src = pmc_traffic(kname) if n == N_MSGS else (None, None)
     result = {
         "metric": "GiB/s device-resident inflate+deflate over batched WS payloads, 1/2/4/8 GPU",
         "value": round(value, 3),
@@ -249,7 +250,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "traffic_source": traffic_src,
-                     "kernel": "inflate_kernel", "kernel_ms": round(kern_ms, 4),
+                     "kernel": kname, "kernel_ms": round(kern_ms, 4),
                      "alg_bytes_per_launch": alg_bytes},
     }
     del src, out, r
