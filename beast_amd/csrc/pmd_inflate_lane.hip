@@ -488,7 +488,11 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
             if (ld) {
                 // 16 bytes from src: the bytes used all lie in [src, cq); the
                 // rest of the 16 may run into the next slot (never stored)
+#ifdef BPMD_EXP_NOHLOAD
+                cw = make_uint4(src, src + 1, src + 2, src + 3);   // timing experiment only
+#else
                 cw = *(const uint4_u*)(o + src);
+#endif
                 cst = true;
             }
         }
