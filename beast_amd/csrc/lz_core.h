@@ -54,10 +54,13 @@ LZ_HD Level level_params(int level)
 // table's 128 at level 6, still within 0.4 % of Beast's output; larger
 // messages keep the table value because their 4 KiB history already costs
 // ratio).
+#ifndef BPMD_CHAIN_CAP
+#define BPMD_CHAIN_CAP 32
+#endif
 LZ_HD unsigned gpu_chain(int level, bool single_chunk)
 {
     const unsigned c = level_params(level).chain;
-    return single_chunk && c > 32 ? 32u : c;
+    return single_chunk && c > BPMD_CHAIN_CAP ? (unsigned)BPMD_CHAIN_CAP : c;
 }
 
 LZ_HD int ilog2(uint32_t v) { return 31 - __builtin_clz(v); }

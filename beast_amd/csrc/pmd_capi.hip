@@ -10,28 +10,36 @@
 #include "../../include/beast_pmd.h"
 
 extern "C" int bpmd_internal_init_fixed(void);
-extern "C" int bpmd_internal_inflate(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
-                                        uint32_t n, uint8_t* out, const uint64_t* out_off,
-                                        const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
-                                        uint32_t raw, hipStream_t stream);
+extern "C" int bpmd_internal_inflate_keyed(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                           uint32_t n, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                                           uint32_t* out_len, int32_t* status, uint32_t raw, const uint32_t* mask_key,
+                                           hipStream_t stream);
 
 extern "C" int bpmd_internal_init_fixed_lane(void);
 extern "C" int bpmd_internal_inflate_lane(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                           uint32_t n, uint8_t* out, const uint64_t* out_off,
-                                          const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
-                                          uint32_t raw, hipStream_t stream);
+                                          const uint32_t* out_cap, uint32_t* out_len, int32_t* status, uint32_t raw,
+                                          const uint32_t* mask_key, const uint32_t* hist_len, uint32_t hist_max,
+                                          hipStream_t stream);
 
-extern "C" int bpmd_internal_deflate(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
-                                     uint32_t n, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
-                                     uint32_t* out_len, int32_t* status, int level, int window_bits, int strategy,
-                                     hipStream_t stream);
+extern "C" int bpmd_internal_deflate_keyed(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                           uint32_t n, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                                           uint32_t* out_len, int32_t* status, int level, int window_bits,
+                                           int strategy, const uint32_t* mask_key, hipStream_t stream);
+
+extern "C" int bpmd_internal_mask(uint8_t* data, const uint64_t* off, const uint32_t* len, uint32_t n,
+                                  const uint32_t* key, const uint8_t* phase, hipStream_t stream);
+extern "C" int bpmd_internal_utf8(const uint8_t* data, const uint64_t* off, const uint32_t* len, uint32_t n,
+                                  int32_t* result, const uint8_t* text, int32_t fail_status, hipStream_t stream);
+extern "C" int bpmd_internal_slide(uint8_t* buf, const uint64_t* base, const uint32_t* pos, const uint32_t* keep,
+                                   uint32_t n, hipStream_t stream);
 
 namespace {
 std::mutex g_init_mu;
 int g_init_device = -1;   // device whose symbols are initialised
 }
 
-extern "C" const char* bpmd_version(void) { return "beast_pmd 0.1 (gfx950)"; }
+extern "C" const char* bpmd_version(void) { return "beast_pmd 0.2 (gfx950)"; }
 
 // Diagnostics only (scripts/diag_*.py): force the launch grid, e.g. one
 // wave, to time a kernel's phases without other waves on the CU.
@@ -83,10 +91,14 @@ extern "C" size_t bpmd_deflate_upper_bound(size_t n)
     return n + ((n + 7) >> 3) + ((n + 63) >> 6) + 11;
 }
 
-extern "C" int bpmd_inflate_batch(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_off,
-                                  const uint32_t* d_in_len, uint32_t n_msgs, uint8_t* d_out,
-                                  const uint64_t* d_out_off, const uint32_t* d_out_cap,
-                                  uint32_t* d_out_len, int32_t* d_status, void* stream)
+namespace {
+
+// bpmd_inflate_batch and its fused / context-takeover forms.  key: masking
+// keys or null; hist: window bytes before each slot (context takeover) or
+// null -- only the lane kernel reads a window, so it always runs then.
+int inflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_off, const uint32_t* d_in_len,
+                 uint32_t n_msgs, uint8_t* d_out, const uint64_t* d_out_off, const uint32_t* d_out_cap,
+                 uint32_t* d_out_len, int32_t* d_status, const uint32_t* key, const uint32_t* hist, void* stream)
 {
     if (!cfg) return BPMD_R_INVALID_ARGUMENT;
     // inflate_stream.ipp:57-61: windowBits outside 8..15 throws domain_error
@@ -97,18 +109,17 @@ extern "C" int bpmd_inflate_batch(const bpmd_cfg* cfg, const uint8_t* d_in, cons
     int r = bpmd_init();
     if (r) return r;
     const uint32_t raw = (cfg->flags & BPMD_F_RAW) ? 1u : 0u;
-    int e = inflate_use_lane(n_msgs)
+    int e = (hist || inflate_use_lane(n_msgs))
                 ? bpmd_internal_inflate_lane(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
-                                             d_status, raw, (hipStream_t)stream)
-                : bpmd_internal_inflate(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
-                                        d_status, raw, (hipStream_t)stream);
+                                             d_status, raw, key, hist, 1u << cfg->window_bits, (hipStream_t)stream)
+                : bpmd_internal_inflate_keyed(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap,
+                                              d_out_len, d_status, raw, key, (hipStream_t)stream);
     return e ? BPMD_R_HIP_ERROR : BPMD_R_OK;
 }
 
-extern "C" int bpmd_deflate_batch(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_off,
-                                  const uint32_t* d_in_len, uint32_t n_msgs, uint8_t* d_out,
-                                  const uint64_t* d_out_off, const uint32_t* d_out_cap,
-                                  uint32_t* d_out_len, int32_t* d_status, void* stream)
+int deflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_off, const uint32_t* d_in_len,
+                 uint32_t n_msgs, uint8_t* d_out, const uint64_t* d_out_off, const uint32_t* d_out_cap,
+                 uint32_t* d_out_len, int32_t* d_status, const uint32_t* key, void* stream)
 {
     if (!cfg) return BPMD_R_INVALID_ARGUMENT;
     // deflate_stream.ipp:235-253: level -1 means 6; windowBits 8 becomes 9;
@@ -124,7 +135,98 @@ extern "C" int bpmd_deflate_batch(const bpmd_cfg* cfg, const uint8_t* d_in, cons
         return BPMD_R_INVALID_ARGUMENT;
     int r = bpmd_init();
     if (r) return r;
-    int e = bpmd_internal_deflate(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
-                                  d_status, level, wbits, cfg->strategy, (hipStream_t)stream);
+    int e = bpmd_internal_deflate_keyed(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
+                                        d_status, level, wbits, cfg->strategy, key, (hipStream_t)stream);
     return e ? BPMD_R_HIP_ERROR : BPMD_R_OK;
+}
+
+}  // namespace
+
+extern "C" int bpmd_inflate_batch(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_off,
+                                  const uint32_t* d_in_len, uint32_t n_msgs, uint8_t* d_out,
+                                  const uint64_t* d_out_off, const uint32_t* d_out_cap,
+                                  uint32_t* d_out_len, int32_t* d_status, void* stream)
+{
+    return inflate_impl(cfg, d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len, d_status,
+                        nullptr, nullptr, stream);
+}
+
+extern "C" int bpmd_deflate_batch(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_off,
+                                  const uint32_t* d_in_len, uint32_t n_msgs, uint8_t* d_out,
+                                  const uint64_t* d_out_off, const uint32_t* d_out_cap,
+                                  uint32_t* d_out_len, int32_t* d_status, void* stream)
+{
+    return deflate_impl(cfg, d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len, d_status,
+                        nullptr, stream);
+}
+
+// ------------------------------------------------ frame passes (§8(f) N1)
+
+extern "C" int bpmd_mask_batch(uint8_t* d_data, const uint64_t* d_off, const uint32_t* d_len, uint32_t n_msgs,
+                               const uint32_t* d_key, const uint8_t* d_phase, void* stream)
+{
+    if (n_msgs == 0) return BPMD_R_OK;
+    if (!d_data || !d_off || !d_len || !d_key) return BPMD_R_INVALID_ARGUMENT;
+    int r = bpmd_init();
+    if (r) return r;
+    return bpmd_internal_mask(d_data, d_off, d_len, n_msgs, d_key, d_phase, (hipStream_t)stream) ? BPMD_R_HIP_ERROR
+                                                                                                 : BPMD_R_OK;
+}
+
+extern "C" int bpmd_utf8_check_batch(const uint8_t* d_data, const uint64_t* d_off, const uint32_t* d_len,
+                                     uint32_t n_msgs, int32_t* d_result, void* stream)
+{
+    if (n_msgs == 0) return BPMD_R_OK;
+    if (!d_data || !d_off || !d_len || !d_result) return BPMD_R_INVALID_ARGUMENT;
+    int r = bpmd_init();
+    if (r) return r;
+    return bpmd_internal_utf8(d_data, d_off, d_len, n_msgs, d_result, nullptr, 0, (hipStream_t)stream)
+               ? BPMD_R_HIP_ERROR
+               : BPMD_R_OK;
+}
+
+extern "C" int bpmd_read_batch(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_off,
+                               const uint32_t* d_in_len, const uint32_t* d_key, const uint8_t* d_text,
+                               uint32_t n_msgs, uint8_t* d_out, const uint64_t* d_out_off,
+                               const uint32_t* d_out_cap, uint32_t* d_out_len, int32_t* d_status, void* stream)
+{
+    int r = inflate_impl(cfg, d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len, d_status,
+                         d_key, nullptr, stream);
+    if (r || n_msgs == 0 || !d_text) return r;
+    // read.hpp:1372-1384: text whose inflated bytes are not UTF-8 fails with bad_frame_payload
+    return bpmd_internal_utf8(d_out, d_out_off, d_out_len, n_msgs, d_status, d_text, BPMD_BAD_FRAME_PAYLOAD,
+                              (hipStream_t)stream)
+               ? BPMD_R_HIP_ERROR
+               : BPMD_R_OK;
+}
+
+extern "C" int bpmd_write_batch(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_off,
+                                const uint32_t* d_in_len, const uint32_t* d_key, uint32_t n_msgs, uint8_t* d_out,
+                                const uint64_t* d_out_off, const uint32_t* d_out_cap, uint32_t* d_out_len,
+                                int32_t* d_status, void* stream)
+{
+    return deflate_impl(cfg, d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len, d_status,
+                        d_key, stream);
+}
+
+// ---------------------------------------------- context takeover (§8(f) N3)
+
+extern "C" int bpmd_inflate_takeover_batch(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_off,
+                                           const uint32_t* d_in_len, const uint32_t* d_hist_len, uint32_t n_msgs,
+                                           uint8_t* d_out, const uint64_t* d_out_off, const uint32_t* d_out_cap,
+                                           uint32_t* d_out_len, int32_t* d_status, void* stream)
+{
+    if (n_msgs && !d_hist_len) return BPMD_R_INVALID_ARGUMENT;
+    return inflate_impl(cfg, d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len, d_status,
+                        nullptr, d_hist_len, stream);
+}
+
+extern "C" int bpmd_slide_batch(uint8_t* d_buf, const uint64_t* d_base, const uint32_t* d_pos, const uint32_t* d_keep,
+                                uint32_t n, void* stream)
+{
+    if (n == 0) return BPMD_R_OK;
+    if (!d_buf || !d_base || !d_pos || !d_keep) return BPMD_R_INVALID_ARGUMENT;
+    int r = bpmd_init();
+    if (r) return r;
+    return bpmd_internal_slide(d_buf, d_base, d_pos, d_keep, n, (hipStream_t)stream) ? BPMD_R_HIP_ERROR : BPMD_R_OK;
 }

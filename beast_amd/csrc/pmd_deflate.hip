@@ -91,6 +91,7 @@ struct Params {
     unsigned max_dist;   // w_size - MIN_LOOKAHEAD
     unsigned chain;      // chain limit (level table, capped for single-chunk messages)
     uint32_t* out_bits;  // optional: payload length in bits before the sync-marker tail
+    const uint32_t* mask_key;   // optional: mask payload i with key i on the way out (write.hpp:679-685)
 };
 
 // Diagnostic build only (-DBPMD_PROF): per-phase wave cycles and counts.
@@ -523,6 +524,7 @@ struct MsgOut {
     uint32_t carry;    // pending partial byte
     unsigned cbits;    // valid bits in carry
     bool overflow;
+    uint32_t key;      // masking key, 0 = unmasked: payload byte j ^= key >> 8 (j % 4) (mask.ipp:38-59)
 };
 
 __device__ __forceinline__ void put_bytes_global(MsgOut& o, const uint8_t* src_lds, unsigned ob, unsigned nbytes)
@@ -534,14 +536,16 @@ __device__ __forceinline__ void put_bytes_global(MsgOut& o, const uint8_t* src_l
     const unsigned wfirst = (ob + 3) >> 2, wlast = end >> 2;   // whole words [wfirst, wlast)
     uint32_t* gw = (uint32_t*)(d - ob);
     const uint32_t* lw = (const uint32_t*)src_lds;
-    for (unsigned k = wfirst + lane; k < wlast; k += WAVE) gw[k] = lw[k];
+    // global dword k holds payload bytes opos - ob + 4k + t: key byte (opos - ob + t) % 4
+    const uint32_t kw = __builtin_amdgcn_alignbit(o.key, o.key, 8u * ((o.opos - ob) & 3u));
+    for (unsigned k = wfirst + lane; k < wlast; k += WAVE) gw[k] = lw[k] ^ kw;
     // edges
     if (lane < 4) {
         const unsigned j = ob + lane;
-        if (j < end && j < wfirst * 4) d[j - ob] = src_lds[j];
+        if (j < end && j < wfirst * 4) d[j - ob] = src_lds[j] ^ (uint8_t)(kw >> (8 * (j & 3)));
     } else if (lane < 8) {
         const unsigned j = wlast * 4 + (lane - 4);
-        if (j >= ob && j < end && j >= wfirst * 4) d[j - ob] = src_lds[j];
+        if (j >= ob && j < end && j >= wfirst * 4) d[j - ob] = src_lds[j] ^ (uint8_t)(kw >> (8 * (j & 3)));
     }
 }
 
@@ -878,15 +882,18 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
         const unsigned total = hb + 4 + clen;
         if (o.opos + total > o.cap) { o.overflow = true; return; }
         uint8_t* d = o.dst + o.opos;
+        // payload byte opos + j takes key byte (opos + j) % 4 (0 = unmasked)
+        const uint32_t kd = __builtin_amdgcn_alignbit(o.key, o.key, 8u * (o.opos & 3u));
+        auto km = [&](unsigned j) { return (uint8_t)(kd >> (8 * (j & 3))); };
         if (lane == 0) {
-            d[0] = (uint8_t)o.carry;
-            if (hb == 2) d[1] = 0;
-            d[hb + 0] = (uint8_t)(clen & 0xFF);
-            d[hb + 1] = (uint8_t)(clen >> 8);
-            d[hb + 2] = (uint8_t)(~clen & 0xFF);
-            d[hb + 3] = (uint8_t)((~clen >> 8) & 0xFF);
+            d[0] = (uint8_t)o.carry ^ km(0);
+            if (hb == 2) d[1] = km(1);
+            d[hb + 0] = (uint8_t)(clen & 0xFF) ^ km(hb);
+            d[hb + 1] = (uint8_t)(clen >> 8) ^ km(hb + 1);
+            d[hb + 2] = (uint8_t)(~clen & 0xFF) ^ km(hb + 2);
+            d[hb + 3] = (uint8_t)((~clen >> 8) & 0xFF) ^ km(hb + 3);
         }
-        for (unsigned i = lane; i < clen; i += WAVE) d[hb + 4 + i] = msg[base + i];
+        for (unsigned i = lane; i < clen; i += WAVE) d[hb + 4 + i] = msg[base + i] ^ km(hb + 4 + i);
         o.opos += total;
         o.carry = 0;
         o.cbits = 0;
@@ -1023,6 +1030,7 @@ deflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
         o.carry = 0;
         o.cbits = 0;
         o.overflow = false;
+        o.key = P.mask_key ? P.mask_key[i] : 0u;
         const uint8_t* msg = in + in_off[i];
         for (uint32_t base = 0; base < len && !o.overflow; base += CHUNK) deflate_chunk<HIST>(S, msg, base, len, P, o, pf);
         // Flush::sync's empty stored block header (000) + pad; 00 00 FF FF stripped
@@ -1030,8 +1038,8 @@ deflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
         if (!o.overflow && o.opos + tb > o.cap) o.overflow = true;
         if (lane == 0) {
             if (!o.overflow) {
-                o.dst[o.opos] = (uint8_t)o.carry;
-                if (tb == 2) o.dst[o.opos + 1] = 0;
+                o.dst[o.opos] = (uint8_t)(o.carry ^ (o.key >> (8 * (o.opos & 3))));
+                if (tb == 2) o.dst[o.opos + 1] = (uint8_t)(o.key >> (8 * ((o.opos + 1) & 3)));
             }
             out_len[i] = o.overflow ? 0u : o.opos + tb;
             if (P.out_bits) P.out_bits[i] = o.overflow ? 0u : o.opos * 8 + o.cbits;
@@ -1065,10 +1073,11 @@ int launch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, ui
 }
 }  // namespace
 
-extern "C" int bpmd_internal_deflate_bits(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
-                                          uint32_t n, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
-                                          uint32_t* out_len, int32_t* status, uint32_t* out_bits, int level,
-                                          int window_bits, int strategy, hipStream_t stream)
+namespace {
+int deflate_impl(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n, uint8_t* out,
+                 const uint64_t* out_off, const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
+                 uint32_t* out_bits, const uint32_t* mask_key, int level, int window_bits, int strategy,
+                 hipStream_t stream)
 {
     bpmd::dfl::Params P;
     P.L = lz::level_params(level);
@@ -1076,11 +1085,31 @@ extern "C" int bpmd_internal_deflate_bits(const uint8_t* in, const uint64_t* in_
     const unsigned wsize = 1u << window_bits;
     P.max_dist = wsize - lz::LOOKAHEAD_MIN;
     P.out_bits = out_bits;
+    P.mask_key = mask_key;
     P.chain = lz::gpu_chain(level, true);
     int e = launch<0>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, P, stream);
     if (e) return e;
     P.chain = lz::gpu_chain(level, false);
     return launch<4096>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, P, stream);
+}
+}  // namespace
+
+extern "C" int bpmd_internal_deflate_bits(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                          uint32_t n, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                                          uint32_t* out_len, int32_t* status, uint32_t* out_bits, int level,
+                                          int window_bits, int strategy, hipStream_t stream)
+{
+    return deflate_impl(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, out_bits, nullptr, level,
+                        window_bits, strategy, stream);
+}
+
+extern "C" int bpmd_internal_deflate_keyed(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                           uint32_t n, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                                           uint32_t* out_len, int32_t* status, int level, int window_bits,
+                                           int strategy, const uint32_t* mask_key, hipStream_t stream)
+{
+    return deflate_impl(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, nullptr, mask_key, level,
+                        window_bits, strategy, stream);
 }
 
 extern "C" int bpmd_internal_deflate(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n,

@@ -105,11 +105,12 @@ struct Msg {
     const uint8_t* p;
     uint32_t n;       // payload bytes
     uint32_t total;   // payload + tail bytes
+    uint32_t key;     // masking key (payload byte i ^= key >> 8 (i % 4), mask.ipp:38-59); 0 = unmasked
 };
 
 __device__ __forceinline__ uint32_t in_byte(const Msg& m, uint32_t i)
 {
-    if (i < m.n) return m.p[i];
+    if (i < m.n) return m.p[i] ^ ((m.key >> (8 * (i & 3))) & 0xffu);
     if (i < m.total) return (i - m.n) >= 2 ? 0xffu : 0u;   // 00 00 FF FF
     return 0;
 }
@@ -122,7 +123,7 @@ __device__ __forceinline__ uint32_t in_word(const Msg& m, uint32_t i)
         const uint32_t* w = (const uint32_t*)(a & ~(uintptr_t)3);
         const unsigned sh = (unsigned)(a & 3) * 8;
         const uint64_t v = ((uint64_t)w[1] << 32) | w[0];
-        return (uint32_t)(v >> sh);
+        return (uint32_t)(v >> sh) ^ __builtin_amdgcn_alignbit(m.key, m.key, 8 * (i & 3));
     }
     return in_byte(m, i) | (in_byte(m, i + 1) << 8) | (in_byte(m, i + 2) << 16) | (in_byte(m, i + 3) << 24);
 }
@@ -151,7 +152,7 @@ __device__ __forceinline__ void load_window(uint32_t* win, const Msg& m, uint32_
 #pragma unroll
         for (unsigned k = 0; k < PER_LANE; ++k) {
             const uint32_t i = lane + k * WAVE;
-            if (i < nfast) win[i] = vals[k];
+            if (i < nfast) win[i] = vals[k] ^ m.key;   // aligned payload: byte j of a word takes key byte j
         }
     }
     for (uint32_t i = nfast + lane; i < NW; i += WAVE) win[i] = in_word(m, wbase + 4 * i);
@@ -844,7 +845,8 @@ __global__ void __launch_bounds__(WAVE)
 inflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                const uint32_t* __restrict__ in_len, uint32_t n_msgs, uint8_t* __restrict__ out,
                const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
-               uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t raw)
+               uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t raw,
+               const uint32_t* __restrict__ mask_key)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     WaveLds& L = *reinterpret_cast<WaveLds*>(smem);
@@ -853,6 +855,7 @@ inflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
         m.p = in + in_off[msg];
         m.n = in_len[msg];
         m.total = m.n + (raw ? 0u : 4u);
+        m.key = mask_key ? mask_key[msg] : 0u;
         Out o;
         o.g = out + out_off[msg];
         o.cap = out_cap[msg];
@@ -875,9 +878,10 @@ inflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
 
 extern "C" unsigned bpmd_diag_grid_override;   // pmd_capi.hip; 0 = size the grid by occupancy
 
-extern "C" int bpmd_internal_inflate(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n,
-                                     uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
-                                     uint32_t* out_len, int32_t* status, uint32_t raw, hipStream_t stream)
+extern "C" int bpmd_internal_inflate_keyed(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                           uint32_t n, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                                           uint32_t* out_len, int32_t* status, uint32_t raw, const uint32_t* mask_key,
+                                           hipStream_t stream)
 {
     using namespace bpmd;
     if (n == 0) return 0;
@@ -889,8 +893,16 @@ extern "C" int bpmd_internal_inflate(const uint8_t* in, const uint64_t* in_off, 
     if (bpmd_diag_grid_override) grid = bpmd_diag_grid_override;
     if (grid > n) grid = n;
     hipLaunchKernelGGL(inflate_kernel, dim3(grid), dim3(WAVE), lds, stream, in, in_off, in_len, n, out, out_off,
-                       out_cap, out_len, status, raw);
+                       out_cap, out_len, status, raw, mask_key);
     return (int)hipGetLastError();
+}
+
+extern "C" int bpmd_internal_inflate(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n,
+                                     uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                                     uint32_t* out_len, int32_t* status, uint32_t raw, hipStream_t stream)
+{
+    return bpmd_internal_inflate_keyed(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, raw, nullptr,
+                                       stream);
 }
 
 extern "C" int bpmd_internal_init_fixed(void)

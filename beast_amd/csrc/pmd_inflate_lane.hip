@@ -51,6 +51,16 @@ constexpr unsigned O_LE = 384;     // u16[16]  litend per code length
 constexpr unsigned O_CLS = 416;    // u8[20]   code-length code symbols, canonical order
 constexpr unsigned O_NIB = 448;    // u8[160]  code lengths, one nibble per symbol
 constexpr unsigned STRIDE = 624;   // 64 * 624 = 39 936 B per wave: 4 waves per CU
+// messages per wave: lanes past LPW idle, so that LPW = 32 puts two waves on
+// every SIMD at 64 Ki messages (BPMD_WPS = 2 caps registers for that occupancy)
+#ifndef BPMD_LPW
+#define BPMD_LPW 64
+#endif
+#ifndef BPMD_WPS
+#define BPMD_WPS 1
+#endif
+constexpr unsigned LPW = BPMD_LPW;
+static_assert(LPW >= 1 && LPW <= 64, "lanes per wave");
 
 #ifndef BPMD_KLIT
 #define BPMD_KLIT 4
@@ -212,11 +222,12 @@ __device__ __forceinline__ uint4 finish_block(uint4 w, uint32_t bi, uint32_t s, 
 // past the payload), or no load at all past E.  The block's dwords are the
 // loaded ones shifted down by m; finish_in() applies that shift and the tail.
 __device__ __forceinline__ uint32_t in_shift(uint32_t b0, uint32_t E) { return b0 + 16 > E ? (b0 + 16 - E) >> 2 : 0u; }
-__device__ __forceinline__ uint4 finish_in(uint4 w, bool ld, uint32_t bi, uint32_t s, uint32_t n, uint32_t tail)
+__device__ __forceinline__ uint4 finish_in(uint4 w, bool ld, uint32_t bi, uint32_t s, uint32_t n, uint32_t tail,
+                                           uint32_t mk)
 {
     const uint32_t b0 = bi * 16;
     const uint32_t E = (s + n + 3) & ~3u;
-    if (!ld) w = make_uint4(0, 0, 0, 0);
+    w = ld ? make_uint4(w.x ^ mk, w.y ^ mk, w.z ^ mk, w.w ^ mk) : make_uint4(0, 0, 0, 0);   // unmask (mk: 0 or the key)
     const uint32_t m = ld ? in_shift(b0, E) : 0u;
     uint4 v = w;
     if (m == 1) v = make_uint4(w.y, w.z, w.w, 0);
@@ -270,20 +281,21 @@ __device__ unsigned long long g_lprof[16];
 #define LP_FLUSH()
 #endif
 
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64, BPMD_WPS)
 inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                     const uint32_t* __restrict__ in_len, uint32_t n_msgs, uint8_t* __restrict__ out,
                     const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
-                    uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t raw)
+                    uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t raw,
+                    const uint32_t* __restrict__ mask_key, const uint32_t* __restrict__ hist_len, uint32_t hist_max)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const unsigned lane = threadIdx.x;
-    const uint32_t msg = blockIdx.x * 64 + lane;
-    uint8_t* T = smem + lane * STRIDE;
+    const uint32_t msg = blockIdx.x * LPW + lane;
+    uint8_t* T = smem + (lane % LPW) * STRIDE;
     uint32_t* H = (uint32_t*)(T + O_HIST);
     uint16_t* LE = (uint16_t*)(T + O_LE);
 
-    const bool valid = msg < n_msgs;
+    const bool valid = lane < LPW && msg < n_msgs;
     const uint8_t* p = in;
     uint32_t n = 0, cap = 0;
     uint8_t* o = out;
@@ -304,10 +316,19 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
     // flat loads would also count on lgkmcnt and stall every LDS wait)
     const uint32_t s = (uint32_t)((uintptr_t)p & 3);
     const uint8_t* A = p - s;
+    // masked payloads (bpmd_read_batch): the dword at A + 4k holds payload
+    // bytes 4k - s .. 4k - s + 3, masked with key bytes (j - s) % 4
+    // (mask.ipp:38-59), so one rotation of the key unmasks every dword
+    const uint32_t mk =
+        (valid && mask_key) ? __builtin_amdgcn_alignbit(mask_key[msg], mask_key[msg], 8u * ((0u - s) & 3u)) : 0u;
+    // context takeover (bpmd_inflate_takeover_batch): the hist bytes before the
+    // slot are the window Beast's inflater keeps across messages
+    const uint32_t hist = (valid && hist_len) ? (hist_len[msg] < hist_max ? hist_len[msg] : hist_max) : 0u;
     uint4 q = make_uint4(0, 0, 0, 0), nx = q, sg = q;
     if (valid) {
-        q = finish_block(issue_block(A, 0, s, n), 0, s, n, tail);
-        nx = finish_block(issue_block(A, 1, s, n), 1, s, n, tail);
+        const uint4 b0w = issue_block(A, 0, s, n), b1w = issue_block(A, 1, s, n);
+        q = finish_block(make_uint4(b0w.x ^ mk, b0w.y ^ mk, b0w.z ^ mk, b0w.w ^ mk), 0, s, n, tail);
+        nx = finish_block(make_uint4(b1w.x ^ mk, b1w.y ^ mk, b1w.z ^ mk, b1w.w ^ mk), 1, s, n, tail);
     }
     // block 2 goes through the same clamped load and finish_in() as the loop's
     const uint32_t E_in = (s + n + 3) & ~3u;
@@ -404,7 +425,7 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
         // (each loaded variable has exactly one load site and is only read
         // here: a second site would merge into a register copy right after
         // the load, i.e. an immediate wait)
-        if (nx_used) nx = finish_in(sg, sg_ld, sg_bi, s, n, tail);
+        if (nx_used) nx = finish_in(sg, sg_ld, sg_bi, s, n, tail, mk);
         if (cst) {
             uint4 w = cw;
             if (cst_pat) {
@@ -452,7 +473,7 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
         if (crem) {
             const uint32_t C = cdist >= 16 ? 16u : 8u;
             bool ld = false;
-            uint32_t src = 0;
+            int32_t src = 0;   // < 0: in the window before the slot
             if (cdist < 8) {
                 const uint32_t adv0 = 8 - 8 % cdist;
                 const uint32_t adv = adv0 < crem ? adv0 : crem;
@@ -464,8 +485,8 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
                     // the cdist bytes before cq, read as 8 bytes that never
                     // start before the slot
                     ld = true;
-                    src = cq >= 8 ? cq - 8 : 0u;
-                    csh = cq - cdist - src;
+                    src = max((int32_t)cq - 8, -(int32_t)hist);
+                    csh = (uint32_t)((int32_t)cq - (int32_t)cdist - src);
                     cst_pat = true;
                     cpd = cdist;
                     csz = 8;
@@ -478,7 +499,7 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
                 // memory section that follows the one that requested it
             } else {
                 ld = true;
-                src = cq - cdist;
+                src = (int32_t)cq - (int32_t)cdist;
                 csz = C;
                 cdst = cq;
                 const uint32_t adv = C < crem ? C : crem;
@@ -600,7 +621,7 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
                     if (raw && pos >= cap) {
                         result = full_status;
                         st = S_DONE;
-                    } else if (is_match && dist > pos) {
+                    } else if (is_match && dist > pos + hist) {
                         result = ST_INVALID_DISTANCE;
                         st = S_DONE;
                     } else if (pos >= cap) {
@@ -981,13 +1002,14 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
 extern "C" int bpmd_internal_inflate_lane(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                           uint32_t n, uint8_t* out, const uint64_t* out_off,
                                           const uint32_t* out_cap, uint32_t* out_len, int32_t* status, uint32_t raw,
+                                          const uint32_t* mask_key, const uint32_t* hist_len, uint32_t hist_max,
                                           hipStream_t stream)
 {
     using namespace bpmd::lpm;
     if (n == 0) return 0;
-    const unsigned grid = (n + 63) / 64;
-    hipLaunchKernelGGL(inflate_lane_kernel, dim3(grid), dim3(64), 64 * STRIDE, stream, in, in_off, in_len, n, out,
-                       out_off, out_cap, out_len, status, raw);
+    const unsigned grid = (n + LPW - 1) / LPW;
+    hipLaunchKernelGGL(inflate_lane_kernel, dim3(grid), dim3(64), LPW * STRIDE, stream, in, in_off, in_len, n, out,
+                       out_off, out_cap, out_len, status, raw, mask_key, hist_len, hist_max);
     return (int)hipGetLastError();
 }
 

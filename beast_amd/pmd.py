@@ -29,6 +29,9 @@ ERRORS = ("ok", "need_buffers", "end_of_stream", "need_dict", "stream_error", "i
           "missing_eob", "invalid_literal_length", "invalid_distance_code", "invalid_distance",
           "over_subscribed_length", "incomplete_length_set", "general")
 F_RAW = 1
+# utf8_checker verdicts (bpmd_utf8) and websocket::error::bad_frame_payload
+UTF8_VALID, UTF8_INCOMPLETE, UTF8_INVALID = 0, 1, 2
+BAD_FRAME_PAYLOAD = 256
 
 
 class BpmdError(RuntimeError):
@@ -56,9 +59,18 @@ def lib():
         L.bpmd_deflate_upper_bound.restype = ctypes.c_size_t
         L.bpmd_inflate_batch.argtypes = [ctypes.POINTER(_Cfg), vp, vp, vp, ctypes.c_uint32, vp, vp, vp, vp, vp, vp]
         L.bpmd_inflate_batch.restype = ctypes.c_int
-        if hasattr(L, "bpmd_deflate_batch"):
-            L.bpmd_deflate_batch.argtypes = [ctypes.POINTER(_Cfg), vp, vp, vp, ctypes.c_uint32, vp, vp, vp, vp, vp, vp]
-            L.bpmd_deflate_batch.restype = ctypes.c_int
+        L.bpmd_deflate_batch.argtypes = [ctypes.POINTER(_Cfg), vp, vp, vp, ctypes.c_uint32, vp, vp, vp, vp, vp, vp]
+        L.bpmd_deflate_batch.restype = ctypes.c_int
+        u32 = ctypes.c_uint32
+        L.bpmd_mask_batch.argtypes = [vp, vp, vp, u32, vp, vp, vp]
+        L.bpmd_utf8_check_batch.argtypes = [vp, vp, vp, u32, vp, vp]
+        L.bpmd_read_batch.argtypes = [ctypes.POINTER(_Cfg), vp, vp, vp, vp, vp, u32, vp, vp, vp, vp, vp, vp]
+        L.bpmd_write_batch.argtypes = [ctypes.POINTER(_Cfg), vp, vp, vp, vp, u32, vp, vp, vp, vp, vp, vp]
+        L.bpmd_inflate_takeover_batch.argtypes = [ctypes.POINTER(_Cfg), vp, vp, vp, vp, u32, vp, vp, vp, vp, vp, vp]
+        L.bpmd_slide_batch.argtypes = [vp, vp, vp, vp, u32, vp]
+        for f in ("bpmd_mask_batch", "bpmd_utf8_check_batch", "bpmd_read_batch", "bpmd_write_batch",
+                  "bpmd_inflate_takeover_batch", "bpmd_slide_batch"):
+            getattr(L, f).restype = ctypes.c_int
         _LIB = L
     return _LIB
 
@@ -197,3 +209,164 @@ def deflate_batch(src: Batch, level: int = 6, window_bits: int = 15, mem_level: 
                                 _ptr(out_off), _ptr(cap), _ptr(out_len), _ptr(status), _stream_handle(stream)),
            "bpmd_deflate_batch")
     return Result(Batch(out, out_off, out_len), cap, status)
+
+
+# ------------------------------------------------------------------------
+# Frame passes
+
+def _optr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _keys(key, n: int, dev):
+    """Per-message 32-bit masking keys (frame-header order, stream_impl.hpp:866-870)
+    as an int32 device tensor holding the same bits; None stays None."""
+    if key is None:
+        return None
+    if isinstance(key, torch.Tensor):
+        if key.dtype == torch.int32:
+            return key.to(dev).contiguous()
+        key = key.cpu().numpy()
+    a = np.array(np.broadcast_to(np.asarray(key, dtype=np.int64) & 0xFFFFFFFF, (n,)), dtype=np.uint32)
+    return torch.from_numpy(a.view(np.int32)).to(dev)
+
+
+def _u8(v, n: int, dev):
+    if v is None:
+        return None
+    if isinstance(v, torch.Tensor):
+        return v.to(device=dev, dtype=torch.uint8).contiguous()
+    a = np.array(np.broadcast_to(np.asarray(v, dtype=np.uint8), (n,)), dtype=np.uint8)
+    return torch.from_numpy(a).to(dev)
+
+
+def mask_batch(b: Batch, key, phase=None, stream=None) -> None:
+    """Beast's mask_inplace (websocket/detail/mask.ipp:38-59) over every message
+    of `b`, in place; `phase` = bytes of the frame already masked, mod 4."""
+    L = lib()
+    dev = b.data.device
+    k = _keys(key, b.n, dev)
+    ph = _u8(phase, b.n, dev)
+    _check(L.bpmd_mask_batch(_ptr(b.data), _ptr(b.off), _ptr(b.len), b.n, _optr(k), _optr(ph),
+                             _stream_handle(stream)), "bpmd_mask_batch")
+
+
+def utf8_check_batch(b: Batch, stream=None, result: torch.Tensor | None = None) -> torch.Tensor:
+    """utf8_checker verdict per message (UTF8_VALID / UTF8_INCOMPLETE / UTF8_INVALID)."""
+    L = lib()
+    res = result if result is not None else torch.empty(b.n, dtype=torch.int32, device=b.data.device)
+    _check(L.bpmd_utf8_check_batch(_ptr(b.data), _ptr(b.off), _ptr(b.len), b.n, _ptr(res), _stream_handle(stream)),
+           "bpmd_utf8_check_batch")
+    return res
+
+
+def _out_slots(n: int, dev, out_cap, out, out_off):
+    if isinstance(out_cap, int):
+        cap = torch.full((n,), out_cap, dtype=torch.int32, device=dev)
+    else:
+        cap = out_cap.to(device=dev, dtype=torch.int32)
+    if out_off is None:
+        out_off = slot_offsets(cap)
+    if out is None:
+        total = int(out_off[-1].item() + cap[-1].item()) if n else 0
+        out = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+    return cap, out, out_off
+
+
+def read_batch(src: Batch, out_cap, key=None, text=None, window_bits: int = 15, raw: bool = False, stream=None,
+               out: torch.Tensor | None = None, out_off: torch.Tensor | None = None) -> Result:
+    """Receive path, fused (read.hpp:1284-1385): unmask with `key` (per message,
+    or None), inflate, and check the output of `text` messages; a text message
+    that is not UTF-8 gets status BAD_FRAME_PAYLOAD.  `src` is not modified."""
+    L = lib()
+    dev = src.data.device
+    n = src.n
+    cap, out, out_off = _out_slots(n, dev, out_cap, out, out_off)
+    k = _keys(key, n, dev)
+    t = _u8(text, n, dev)
+    out_len = torch.empty(n, dtype=torch.int32, device=dev)
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+    cfg = _Cfg(0, window_bits, 8, 0, F_RAW if raw else 0)
+    _check(L.bpmd_read_batch(ctypes.byref(cfg), _ptr(src.data), _ptr(src.off), _ptr(src.len), _optr(k), _optr(t), n,
+                             _ptr(out), _ptr(out_off), _ptr(cap), _ptr(out_len), _ptr(status), _stream_handle(stream)),
+           "bpmd_read_batch")
+    return Result(Batch(out, out_off, out_len), cap, status)
+
+
+def write_batch(src: Batch, key=None, level: int = 6, window_bits: int = 15, mem_level: int = 4, strategy: int = 0,
+                stream=None, out_cap=None, out: torch.Tensor | None = None,
+                out_off: torch.Tensor | None = None) -> Result:
+    """Send path, fused (write.hpp:655-703): deflate_batch with each payload
+    masked by `key` in the kernel's output stores (client role)."""
+    L = lib()
+    dev = src.data.device
+    n = src.n
+    if out_cap is None:
+        ln = src.len.to(torch.int64)
+        out_cap = (ln + (ln + 7) // 8 + (ln + 63) // 64 + 11).to(torch.int32)
+    cap, out, out_off = _out_slots(n, dev, out_cap, out, out_off)
+    k = _keys(key, n, dev)
+    out_len = torch.empty(n, dtype=torch.int32, device=dev)
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+    cfg = _Cfg(level, window_bits, mem_level, strategy, 0)
+    _check(L.bpmd_write_batch(ctypes.byref(cfg), _ptr(src.data), _ptr(src.off), _ptr(src.len), _optr(k), n,
+                              _ptr(out), _ptr(out_off), _ptr(cap), _ptr(out_len), _ptr(status),
+                              _stream_handle(stream)), "bpmd_write_batch")
+    return Result(Batch(out, out_off, out_len), cap, status)
+
+
+# ------------------------------------------------------------------------
+# Context takeover (SURVEY.md §8(f) N3)
+
+class TakeoverInflater:
+    """Receive side of context-takeover connections: Beast's inflater keeps its
+    window across messages (impl_base.hpp:192-202; inflate_stream::clear() is a
+    no-op, inflate_stream.ipp:49-53).  Each connection owns a device buffer of
+    2 * 2^window_bits + max_msg bytes holding its latest output; message k of a
+    connection is decoded right after its earlier output, whose last
+    2^window_bits bytes are the window.  When a buffer cannot take the next
+    message, its window slides to the front on the device (bpmd_slide_batch).
+    Bookkeeping stays on the device except for that fullness test."""
+
+    def __init__(self, n_conn: int, window_bits: int = 15, max_msg: int = 1 << 16, device="cuda"):
+        self.wbits = window_bits
+        self.W = 1 << window_bits
+        self.max_msg = max_msg
+        self.slot = (2 * self.W + max_msg + 15) // 16 * 16
+        self.buf = torch.zeros(n_conn * self.slot + 16, dtype=torch.uint8, device=device)
+        self.base = torch.arange(n_conn, dtype=torch.int64, device=device) * self.slot
+        self.pos = torch.zeros(n_conn, dtype=torch.int64, device=device)
+
+    def inflate(self, src: Batch, out_cap, conn=None, stream=None) -> Result:
+        """Inflate src's messages, message i continuing connection conn[i]
+        (default i); at most one message per connection per call."""
+        L = lib()
+        dev = self.buf.device
+        n = src.n
+        conn = torch.arange(n, device=dev) if conn is None else torch.as_tensor(conn, device=dev).long()
+        cap = torch.full((n,), out_cap, dtype=torch.int32, device=dev) if isinstance(out_cap, int) \
+            else out_cap.to(device=dev, dtype=torch.int32)
+        if int(cap.max().item() if n else 0) > self.max_msg:
+            raise BpmdError("out_cap exceeds max_msg")
+        pos = self.pos[conn]
+        full = pos + cap.to(torch.int64) > self.slot
+        if n and bool(full.any()):
+            idx = conn[full]
+            keep = torch.minimum(self.pos[idx], torch.tensor(self.W, device=dev))
+            p32 = self.pos[idx].to(torch.int32)
+            k32 = keep.to(torch.int32)
+            b64 = self.base[idx].contiguous()
+            _check(L.bpmd_slide_batch(_ptr(self.buf), _ptr(b64), _ptr(p32), _ptr(k32), int(idx.numel()),
+                                      _stream_handle(stream)), "bpmd_slide_batch")
+            self.pos[idx] = keep
+            pos = self.pos[conn]
+        hist = torch.minimum(pos, torch.tensor(self.W, device=dev)).to(torch.int32)
+        out_off = (self.base[conn] + pos).contiguous()
+        out_len = torch.empty(n, dtype=torch.int32, device=dev)
+        status = torch.empty(n, dtype=torch.int32, device=dev)
+        cfg = _Cfg(0, self.wbits, 8, 0, 0)
+        _check(L.bpmd_inflate_takeover_batch(ctypes.byref(cfg), _ptr(src.data), _ptr(src.off), _ptr(src.len),
+                                             _ptr(hist), n, _ptr(self.buf), _ptr(out_off), _ptr(cap), _ptr(out_len),
+                                             _ptr(status), _stream_handle(stream)), "bpmd_inflate_takeover_batch")
+        self.pos[conn] = pos + out_len.to(torch.int64)
+        return Result(Batch(self.buf, out_off, out_len), cap, status)

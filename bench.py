@@ -184,6 +184,7 @@ def main():
     ap.add_argument("--msgs", type=int, default=N_MSGS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-deflate", action="store_true")
+    ap.add_argument("--no-frame", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -253,6 +254,56 @@ def main():
                      "kernel": kname, "kernel_ms": round(kern_ms, 4),
                      "alg_bytes_per_launch": alg_bytes},
     }
+
+    # ---------------------------------- N1 frame passes on the same C2 batch
+    if not args.no_frame:
+        g = torch.Generator().manual_seed(0x5EED0011 + rank)
+        keys = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, generator=g).to(dev)
+        text = torch.ones(n, dtype=torch.uint8, device=dev)
+        msrc = pmd.Batch(src.data.clone(), src.off, src.len)
+        pmd.mask_batch(msrc, keys)   # the clients' masked frames
+
+        def read_step():
+            return pmd.read_batch(msrc, cap, key=keys, text=text, out=out, out_off=out_off)
+
+        rr = read_step()
+        torch.cuda.synchronize()
+        ref_dev = torch.from_numpy(raw.reshape(n, MSG_BYTES)).to(dev)
+        okr = int((rr.status != 0).sum()) == 0 and torch.equal(out[: n * MSG_BYTES].view(n, MSG_BYTES), ref_dev)
+        r_step, _ = timer.run(read_step, args.steps, args.warmup)
+        ob = pmd.Batch(out, out_off, rr.out.len)
+        ures = torch.empty(n, dtype=torch.int32, device=dev)
+
+        def utf8_step():
+            return pmd.utf8_check_batch(ob, result=ures)
+
+        u_step, u_kern = timer.run(utf8_step, args.steps, args.warmup)
+        oku = int((ures != 0).sum()) == 0
+
+        def mask_step():
+            pmd.mask_batch(msrc, keys)
+
+        m_step, m_kern = timer.run(mask_step, args.steps, args.warmup)
+        result["frame"] = {
+            "workload": "C2 payloads as masked client text frames: fused unmask+inflate+UTF-8 (bpmd_read_batch); "
+                        "UTF-8 check of the 256 MiB inflated batch; in-place mask of the compressed batch",
+            "read_value": round(uncomp * world / (1 << 30) / r_step, 3), "read_ms_per_step": round(r_step * 1e3, 4),
+            "read_ok": bool(okr),
+            "utf8_value": round(uncomp * world / (1 << 30) / u_step, 3), "utf8_ok": bool(oku),
+            "utf8_roofline": {"bound": "hbm", "achieved": round((uncomp + 16 * n) / (u_kern * 1e-3) / 1e9, 2),
+                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": round((uncomp + 16 * n) / (u_kern * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                              "kernel": "utf8_kernel", "kernel_ms": round(u_kern, 4)},
+            "mask_value": round(comp * world / (1 << 30) / m_step, 3),
+            "mask_roofline": {"bound": "hbm", "achieved": round((2 * comp + 16 * n) / (m_kern * 1e-3) / 1e9, 2),
+                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": round((2 * comp + 16 * n) / (m_kern * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                              "kernel": "mask_kernel", "kernel_ms": round(m_kern, 4)},
+            "unit": "GiB/s (mask: of compressed bytes)",
+        }
+        if not (okr and oku):
+            log(f"[rank {rank}] FRAME PARITY FAILURE read={okr} utf8={oku}")
+        del msrc, ob, rr
     del src, out, r
 
     # ------------------------------------------------- C3 deflate round trip

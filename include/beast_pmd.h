@@ -128,6 +128,82 @@ int bpmd_set_inflate_kernel(int mode);
 size_t bpmd_deflate_upper_bound(size_t n);
 
 /* ---------------------------------------------------------------------
+ * Frame-adjacent byte passes.  Masking keys are the
+ * frame header's 32-bit key as Beast reads it, little-endian from the wire
+ * (stream_impl.hpp:866-870): payload byte j is XORed with byte (j + phase) % 4
+ * of the key (prepare_key / mask_inplace, websocket/detail/mask.ipp:20-59).
+ * ------------------------------------------------------------------- */
+
+/* Batched mask_inplace (mask.ipp:38-59), in place.  d_phase[i] is the key
+ * rotation a prepared_key carries after masking the frame's earlier bytes
+ * (rol, mask.ipp:29-36), i.e. their count mod 4; NULL = 0.  Masking is an
+ * involution: the same call masks (write.hpp:679-685) and unmasks
+ * (read.hpp:1324-1327). */
+int bpmd_mask_batch(uint8_t* d_data, const uint64_t* d_off, const uint32_t* d_len, uint32_t n_msgs,
+                    const uint32_t* d_key, const uint8_t* d_phase, void* stream);
+
+/* utf8_checker verdicts (websocket/detail/utf8_checker.ipp) */
+enum bpmd_utf8 {
+    BPMD_UTF8_VALID = 0,       /* write() and finish() succeed */
+    BPMD_UTF8_INCOMPLETE = 1,  /* write() succeeds, finish() fails: ends inside a code point */
+    BPMD_UTF8_INVALID = 2      /* write() fails */
+};
+
+/* Batched check_utf8 (utf8_checker.ipp:317-324) keeping the verdict of one
+ * utf8_checker::write() over each whole message: d_result[i] = bpmd_utf8.
+ * Feeding a message in pieces gives the same verdicts: the fail-fast rule
+ * (utf8_checker.ipp:86-157) rejects exactly the invalid prefixes. */
+int bpmd_utf8_check_batch(const uint8_t* d_data, const uint64_t* d_off, const uint32_t* d_len, uint32_t n_msgs,
+                          int32_t* d_result, void* stream);
+
+/* websocket::error::bad_frame_payload (websocket/error.hpp): the per-message
+ * status bpmd_read_batch reports for a text message that is not UTF-8. */
+#define BPMD_BAD_FRAME_PAYLOAD 256
+
+/* Receive side of a batch of permessage-deflate messages, fused
+ * (read.hpp:1284-1385): unmask the payload inside inflate's input loads
+ * (server role, read.hpp:1324-1327; d_key NULL = unmasked), inflate as
+ * bpmd_inflate_batch, then check the inflated bytes of text messages
+ * (d_text[i] != 0; NULL = all binary) as read.hpp:1372-1384 does.
+ * d_status[i]: inflate's zlib::error if nonzero, else BPMD_BAD_FRAME_PAYLOAD
+ * for a text message that is not valid UTF-8, else 0.  d_in is not
+ * modified. */
+int bpmd_read_batch(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_off, const uint32_t* d_in_len,
+                    const uint32_t* d_key, const uint8_t* d_text, uint32_t n_msgs, uint8_t* d_out,
+                    const uint64_t* d_out_off, const uint32_t* d_out_cap, uint32_t* d_out_len, int32_t* d_status,
+                    void* stream);
+
+/* Send side, fused (write.hpp:655-703): deflate as bpmd_deflate_batch and
+ * mask each payload with d_key[i] inside the kernel's output stores (client
+ * role, write.hpp:679-685; d_key NULL = unmasked). */
+int bpmd_write_batch(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_off, const uint32_t* d_in_len,
+                     const uint32_t* d_key, uint32_t n_msgs, uint8_t* d_out, const uint64_t* d_out_off,
+                     const uint32_t* d_out_cap, uint32_t* d_out_len, int32_t* d_status, void* stream);
+
+/* ---------------------------------------------------------------------
+ * Context takeover: when no_context_takeover is not
+ * negotiated, Beast's inflater keeps its window from message to message
+ * (do_context_takeover_read -> inflate_stream::clear() is a no-op,
+ * impl_base.hpp:192-202, inflate_stream.ipp:49-53), so a message may copy
+ * from the connection's earlier output.  Each connection keeps its output in
+ * one device buffer; message i is decoded into d_out + d_out_off[i], right
+ * after that connection's earlier output, whose last d_hist_len[i] bytes
+ * (clamped to 2^windowBits) are the window.  One message per connection per
+ * batch; connections run in parallel.  Statuses as bpmd_inflate_batch
+ * (invalid_distance for a distance past the window).
+ * ------------------------------------------------------------------- */
+int bpmd_inflate_takeover_batch(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_off,
+                                const uint32_t* d_in_len, const uint32_t* d_hist_len, uint32_t n_msgs,
+                                uint8_t* d_out, const uint64_t* d_out_off, const uint32_t* d_out_cap,
+                                uint32_t* d_out_len, int32_t* d_status, void* stream);
+
+/* Window maintenance for the buffers above: move the d_keep[i] bytes before
+ * d_pos[i] of the buffer at d_buf + d_base[i] to its front (the caller slides
+ * only when d_pos[i] >= 2 * d_keep[i], so the ranges never overlap). */
+int bpmd_slide_batch(uint8_t* d_buf, const uint64_t* d_base, const uint32_t* d_pos, const uint32_t* d_keep,
+                     uint32_t n, void* stream);
+
+/* ---------------------------------------------------------------------
  * Per-stream API behind the C++ compatibility facade
  * (include/beast_amd/zlib.hpp).  Host buffers; each call runs the batch
  * kernels on the current device for one message and synchronises.

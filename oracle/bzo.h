@@ -120,6 +120,24 @@ int bzo_pmd_inflate_batch(int window_bits, int raw, const uint8_t* in,
                           const uint64_t* out_off, const uint32_t* out_cap,
                           uint32_t* out_len, int32_t* status, int threads);
 
+/* ---- frame-adjacent byte passes (bzo_frame.c) ---- */
+/* mask_inplace (websocket/detail/mask.ipp:38-59) with a key already rotated
+ * by `phase` bytes; returns the rotation afterwards */
+unsigned bzo_mask(uint8_t* p, size_t n, uint32_t key, unsigned phase);
+/* utf8_checker (websocket/detail/utf8_checker.hpp/.ipp) */
+typedef struct bzo_utf8 {
+    size_t need;   /* bytes still needed by the open code point */
+    size_t have;   /* bytes of it seen */
+    uint8_t cp[4];
+} bzo_utf8;
+void bzo_utf8_reset(bzo_utf8*);
+int  bzo_utf8_write(bzo_utf8*, const uint8_t* in, size_t n);
+int  bzo_utf8_finish(bzo_utf8*);
+/* one write() + finish(): 0 valid, 1 write ok but finish fails, 2 write fails */
+int  bzo_utf8_check(const uint8_t* p, size_t n);
+int  bzo_utf8_check_batch(const uint8_t* in, const uint64_t* off, const uint32_t* len, uint32_t n,
+                          int32_t* result);
+
 #ifdef __cplusplus
 }
 #endif

@@ -68,6 +68,13 @@ def lib():
         vp = ctypes.c_void_p
         L.bzo_pmd_deflate_batch.argtypes = [ctypes.c_int] * 4 + [vp] * 3 + [ctypes.c_uint32] + [vp] * 5 + [ctypes.c_int]
         L.bzo_pmd_inflate_batch.argtypes = [ctypes.c_int, ctypes.c_int] + [vp] * 3 + [ctypes.c_uint32] + [vp] * 5 + [ctypes.c_int]
+        L.bzo_mask.argtypes = [vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint]
+        L.bzo_mask.restype = ctypes.c_uint
+        L.bzo_utf8_reset.argtypes = [vp]
+        L.bzo_utf8_write.argtypes = [vp, ctypes.c_char_p, ctypes.c_size_t]
+        L.bzo_utf8_finish.argtypes = [vp]
+        L.bzo_utf8_check.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+        L.bzo_utf8_check_batch.argtypes = [vp, vp, vp, ctypes.c_uint32, vp]
         _LIB = L
     return _LIB
 
@@ -238,3 +245,89 @@ class Deflater:
             self.L.bzo_deflate_free(self.z)
         except Exception:
             pass
+
+
+# ---------------------------------------------------------------- frame passes
+
+def mask(data: bytes, key: int, phase: int = 0) -> bytes:
+    """mask_inplace (websocket/detail/mask.ipp:38-59) with the frame key
+    (little-endian from the wire) rotated by `phase` bytes already masked."""
+    data = bytes(data)
+    buf = ctypes.create_string_buffer(data, max(len(data), 1))
+    lib().bzo_mask(buf, len(data), key & 0xFFFFFFFF, phase & 3)
+    return buf.raw[:len(data)]
+
+
+def utf8_check(data: bytes) -> int:
+    """0 valid, 1 write() ok but finish() fails, 2 write() fails (utf8_checker.ipp)."""
+    data = bytes(data)
+    return lib().bzo_utf8_check(data, len(data))
+
+
+class _U8(ctypes.Structure):
+    _fields_ = [("need", ctypes.c_size_t), ("have", ctypes.c_size_t), ("cp", ctypes.c_uint8 * 4)]
+
+
+class Utf8Checker:
+    """Streaming utf8_checker (websocket/detail/utf8_checker.hpp:29-86)."""
+
+    def __init__(self):
+        self._s = _U8()
+        lib().bzo_utf8_reset(ctypes.byref(self._s))
+
+    def write(self, data) -> bool:
+        data = bytes(data)
+        return bool(lib().bzo_utf8_write(ctypes.byref(self._s), data, len(data)))
+
+    def finish(self) -> bool:
+        return bool(lib().bzo_utf8_finish(ctypes.byref(self._s)))
+
+    def reset(self):
+        lib().bzo_utf8_reset(ctypes.byref(self._s))
+
+
+# ------------------------------------------------------------ context takeover
+
+def pmd_deflate_stream(msgs, level=6, wbits=15, mem_level=4, strategy=0):
+    """One connection without no_context_takeover: one deflater for every
+    message, never reset (impl_base.hpp:85-166).  Returns the payloads."""
+    L = lib()
+    z = L.bzo_deflate_new()
+    try:
+        if L.bzo_deflate_reset_params(z, level, wbits, mem_level, strategy):
+            raise ValueError("invalid deflate parameters")
+        out = []
+        for m in msgs:
+            m = bytes(m)
+            cap = upper_bound(len(m)) + 64
+            buf = ctypes.create_string_buffer(cap)
+            src = ctypes.create_string_buffer(m, len(m)) if m else None
+            n = L.bzo_pmd_deflate_msg(z, src, len(m), buf, cap)
+            if n < 0:
+                raise RuntimeError(f"deflate failed: {ERRORS.get(-n, -n)}")
+            out.append(buf.raw[:n])
+        return out
+    finally:
+        L.bzo_deflate_free(z)
+
+
+def pmd_inflate_stream(payloads, cap: int = 1 << 20, wbits=15):
+    """One connection's messages through one inflater that keeps its window
+    (inflate_stream::clear() is a no-op, inflate_stream.ipp:49-53).  Returns
+    [(status, output)]."""
+    L = lib()
+    z = L.bzo_inflate_new()
+    try:
+        if L.bzo_inflate_reset(z, wbits):
+            raise ValueError("windowBits out of range")
+        res = []
+        for p in payloads:
+            p = bytes(p)
+            out = ctypes.create_string_buffer(max(cap, 1))
+            got = ctypes.c_size_t(0)
+            src = ctypes.create_string_buffer(p, len(p)) if p else None
+            st = L.bzo_pmd_inflate_msg(z, src, len(p), out, cap, ctypes.byref(got), 0)
+            res.append((st, out.raw[:got.value]))
+        return res
+    finally:
+        L.bzo_inflate_free(z)
