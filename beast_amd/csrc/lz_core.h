@@ -55,7 +55,7 @@ LZ_HD Level level_params(int level)
 // messages keep the table value because their 4 KiB history already costs
 // ratio).
 #ifndef BPMD_CHAIN_CAP
-#define BPMD_CHAIN_CAP 32
+#define BPMD_CHAIN_CAP 4
 #endif
 LZ_HD unsigned gpu_chain(int level, bool single_chunk)
 {

@@ -68,7 +68,13 @@ def lib():
         L.bpmd_write_batch.argtypes = [ctypes.POINTER(_Cfg), vp, vp, vp, vp, u32, vp, vp, vp, vp, vp, vp]
         L.bpmd_inflate_takeover_batch.argtypes = [ctypes.POINTER(_Cfg), vp, vp, vp, vp, u32, vp, vp, vp, vp, vp, vp]
         L.bpmd_slide_batch.argtypes = [vp, vp, vp, vp, u32, vp]
-        for f in ("bpmd_mask_batch", "bpmd_utf8_check_batch", "bpmd_read_batch", "bpmd_write_batch",
+        L.bpmd_batcher_create.argtypes = [ctypes.POINTER(_Cfg), ctypes.c_int, u32, ctypes.c_size_t, ctypes.c_size_t,
+                                          u32, ctypes.POINTER(vp)]
+        L.bpmd_batcher_submit.argtypes = [vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t, vp, vp]
+        L.bpmd_batcher_flush.argtypes = [vp]
+        L.bpmd_batcher_destroy.argtypes = [vp]
+        L.bpmd_batcher_destroy.restype = None
+        for f in ("bpmd_batcher_create", "bpmd_batcher_submit", "bpmd_batcher_flush", "bpmd_mask_batch", "bpmd_utf8_check_batch", "bpmd_read_batch", "bpmd_write_batch",
                   "bpmd_inflate_takeover_batch", "bpmd_slide_batch"):
             getattr(L, f).restype = ctypes.c_int
         _LIB = L
@@ -370,3 +376,82 @@ class TakeoverInflater:
                                              _ptr(status), _stream_handle(stream)), "bpmd_inflate_takeover_batch")
         self.pos[conn] = pos + out_len.to(torch.int64)
         return Result(Batch(self.buf, out_off, out_len), cap, status)
+
+
+# ------------------------------------------------------------------------
+# Cross-connection micro-batcher
+
+_DONE = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int32, ctypes.c_size_t)
+
+
+class Completion:
+    """Result of one submitted message: wait() returns (status, bytes)."""
+
+    def __init__(self, cap: int):
+        import threading
+        self.buf = ctypes.create_string_buffer(max(cap, 1))
+        self.cap = cap
+        self.event = threading.Event()
+        self.status = None
+        self.length = 0
+
+    def wait(self, timeout=None):
+        if not self.event.wait(timeout):
+            raise TimeoutError("message not completed")
+        return self.status, self.buf.raw[:self.length]
+
+
+class Batcher:
+    """Host-buffer front end that coalesces single messages from many
+    connections (threads) into batch launches (bpmd_batcher_*)."""
+
+    def __init__(self, op: str = "inflate", level: int = 6, window_bits: int = 15, mem_level: int = 4,
+                 strategy: int = 0, raw: bool = False, max_msgs: int = 4096, max_in_bytes: int = 16 << 20,
+                 max_out_bytes: int = 64 << 20, max_delay_us: int = 200):
+        import threading
+        self.L = lib()
+        self.op = op
+        cfg = _Cfg(level, window_bits, mem_level, strategy, F_RAW if raw else 0)
+        h = ctypes.c_void_p()
+        _check(self.L.bpmd_batcher_create(ctypes.byref(cfg), 0 if op == "inflate" else 1, max_msgs, max_in_bytes,
+                                          max_out_bytes, max_delay_us, ctypes.byref(h)), "bpmd_batcher_create")
+        self._h = h
+        self._lock = threading.Lock()
+        self._pending = {}
+        self._next = 1
+        self._cb = _DONE(self._done)
+
+    def _done(self, user, status, n):
+        with self._lock:
+            c = self._pending.pop(user)
+        c.status, c.length = int(status), int(n)
+        c.event.set()
+
+    def submit(self, data: bytes, out_cap: int) -> Completion:
+        data = bytes(data)
+        c = Completion(out_cap)
+        with self._lock:
+            key = self._next
+            self._next += 1
+            self._pending[key] = c
+        src = ctypes.create_string_buffer(data, max(len(data), 1))
+        r = self.L.bpmd_batcher_submit(self._h, src, len(data), c.buf, out_cap, self._cb, ctypes.c_void_p(key))
+        if r:
+            with self._lock:
+                self._pending.pop(key, None)
+            _check(r, "bpmd_batcher_submit")
+        return c
+
+    def flush(self):
+        _check(self.L.bpmd_batcher_flush(self._h), "bpmd_batcher_flush")
+
+    def close(self):
+        if self._h:
+            self.L.bpmd_batcher_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

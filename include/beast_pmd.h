@@ -197,6 +197,37 @@ int bpmd_inflate_takeover_batch(const bpmd_cfg* cfg, const uint8_t* d_in, const 
                                 uint8_t* d_out, const uint64_t* d_out_off, const uint32_t* d_out_cap,
                                 uint32_t* d_out_len, int32_t* d_status, void* stream);
 
+/* ---------------------------------------------------------------------
+ * Cross-connection micro-batcher.  Beast runs one codec
+ * call per message inside each connection's async operation
+ * (write_some_op, write.hpp:463-545; read.hpp:522-610 via impl_base.hpp:85-190);
+ * the batcher coalesces those calls across connections: any thread submits
+ * one message (host bytes, copied at submit) with a completion callback;
+ * batches launch when max_msgs or the staging bytes fill up, or when the
+ * oldest message has waited max_delay_us.  Two pinned staging slots
+ * alternate, so submissions continue while the GPU works.
+ * ------------------------------------------------------------------- */
+enum bpmd_op { BPMD_OP_INFLATE = 0, BPMD_OP_DEFLATE = 1 };
+typedef struct bpmd_batcher bpmd_batcher;
+/* One message done (on the batcher's completion thread; it must not call
+ * bpmd_batcher_flush or _destroy).  status: the message's zlib::error
+ * (need_buffers: out_cap too small), or a negative bpmd_result when its batch
+ * failed; out_len: bytes written to the submitter's out buffer. */
+typedef void (*bpmd_done_fn)(void* user, int32_t status, size_t out_len);
+/* cfg as for bpmd_inflate_batch / bpmd_deflate_batch (validated the same
+ * way); max_in_bytes / max_out_bytes size each staging slot (input bytes; for
+ * inflate the sum of out_cap, for deflate of deflate_upper_bound(n)). */
+int bpmd_batcher_create(const bpmd_cfg* cfg, int op, uint32_t max_msgs, size_t max_in_bytes, size_t max_out_bytes,
+                        uint32_t max_delay_us, bpmd_batcher** out);
+/* Queue one message.  `out` must stay valid until fn runs. */
+int bpmd_batcher_submit(bpmd_batcher* b, const void* in, size_t n, void* out, size_t out_cap, bpmd_done_fn fn,
+                        void* user);
+/* Launch what is queued and wait until every message submitted so far has
+ * completed. */
+int bpmd_batcher_flush(bpmd_batcher* b);
+/* Completes everything queued, then frees the batcher. */
+void bpmd_batcher_destroy(bpmd_batcher* b);
+
 /* Window maintenance for the buffers above: move the d_keep[i] bytes before
  * d_pos[i] of the buffer at d_buf + d_base[i] to its front (the caller slides
  * only when d_pos[i] >= 2 * d_keep[i], so the ranges never overlap). */
