@@ -27,6 +27,12 @@ extern "C" int bpmd_internal_deflate_keyed(const uint8_t* in, const uint64_t* in
                                            uint32_t* out_len, int32_t* status, int level, int window_bits,
                                            int strategy, const uint32_t* mask_key, hipStream_t stream);
 
+extern "C" int bpmd_internal_deflate_takeover(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                              uint32_t n, uint8_t* out, const uint64_t* out_off,
+                                              const uint32_t* out_cap, uint32_t* out_len, int32_t* status, int level,
+                                              int window_bits, int strategy, const uint32_t* hist_len,
+                                              hipStream_t stream);
+
 extern "C" int bpmd_internal_mask(uint8_t* data, const uint64_t* off, const uint32_t* len, uint32_t n,
                                   const uint32_t* key, const uint8_t* phase, hipStream_t stream);
 extern "C" int bpmd_internal_utf8(const uint8_t* data, const uint64_t* off, const uint32_t* len, uint32_t n,
@@ -119,7 +125,7 @@ int inflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
 
 int deflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_off, const uint32_t* d_in_len,
                  uint32_t n_msgs, uint8_t* d_out, const uint64_t* d_out_off, const uint32_t* d_out_cap,
-                 uint32_t* d_out_len, int32_t* d_status, const uint32_t* key, void* stream)
+                 uint32_t* d_out_len, int32_t* d_status, const uint32_t* key, const uint32_t* hist, void* stream)
 {
     if (!cfg) return BPMD_R_INVALID_ARGUMENT;
     // deflate_stream.ipp:235-253: level -1 means 6; windowBits 8 becomes 9;
@@ -135,8 +141,12 @@ int deflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
         return BPMD_R_INVALID_ARGUMENT;
     int r = bpmd_init();
     if (r) return r;
-    int e = bpmd_internal_deflate_keyed(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
-                                        d_status, level, wbits, cfg->strategy, key, (hipStream_t)stream);
+    int e = hist ? bpmd_internal_deflate_takeover(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap,
+                                                  d_out_len, d_status, level, wbits, cfg->strategy, hist,
+                                                  (hipStream_t)stream)
+                 : bpmd_internal_deflate_keyed(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap,
+                                               d_out_len, d_status, level, wbits, cfg->strategy, key,
+                                               (hipStream_t)stream);
     return e ? BPMD_R_HIP_ERROR : BPMD_R_OK;
 }
 
@@ -157,7 +167,7 @@ extern "C" int bpmd_deflate_batch(const bpmd_cfg* cfg, const uint8_t* d_in, cons
                                   uint32_t* d_out_len, int32_t* d_status, void* stream)
 {
     return deflate_impl(cfg, d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len, d_status,
-                        nullptr, stream);
+                        nullptr, nullptr, stream);
 }
 
 // ------------------------------------------------ frame passes (§8(f) N1)
@@ -206,7 +216,7 @@ extern "C" int bpmd_write_batch(const bpmd_cfg* cfg, const uint8_t* d_in, const 
                                 int32_t* d_status, void* stream)
 {
     return deflate_impl(cfg, d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len, d_status,
-                        d_key, stream);
+                        d_key, nullptr, stream);
 }
 
 // ---------------------------------------------- context takeover (§8(f) N3)
@@ -218,6 +228,16 @@ extern "C" int bpmd_inflate_takeover_batch(const bpmd_cfg* cfg, const uint8_t* d
 {
     if (n_msgs && !d_hist_len) return BPMD_R_INVALID_ARGUMENT;
     return inflate_impl(cfg, d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len, d_status,
+                        nullptr, d_hist_len, stream);
+}
+
+extern "C" int bpmd_deflate_takeover_batch(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_off,
+                                           const uint32_t* d_in_len, const uint32_t* d_hist_len, uint32_t n_msgs,
+                                           uint8_t* d_out, const uint64_t* d_out_off, const uint32_t* d_out_cap,
+                                           uint32_t* d_out_len, int32_t* d_status, void* stream)
+{
+    if (n_msgs && !d_hist_len) return BPMD_R_INVALID_ARGUMENT;
+    return deflate_impl(cfg, d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len, d_status,
                         nullptr, d_hist_len, stream);
 }
 

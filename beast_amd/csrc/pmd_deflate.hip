@@ -92,6 +92,7 @@ struct Params {
     unsigned chain;      // chain limit (level table, capped for single-chunk messages)
     uint32_t* out_bits;  // optional: payload length in bits before the sync-marker tail
     const uint32_t* mask_key;   // optional: mask payload i with key i on the way out (write.hpp:679-685)
+    const uint32_t* hist_len;   // optional (context takeover): plaintext bytes before message i usable as history
 };
 
 // Diagnostic build only (-DBPMD_PROF): per-phase wave cycles and counts.
@@ -550,14 +551,18 @@ __device__ __forceinline__ void put_bytes_global(MsgOut& o, const uint8_t* src_l
 }
 
 template <int HIST>
-__device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base, unsigned len, const Params& P,
-                              MsgOut& o, Prof& pf)
+__device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base, unsigned len, unsigned hist,
+                              const Params& P, MsgOut& o, Prof& pf)
 {
     using namespace lz;
     const unsigned lane = lane_id();
     const unsigned cend = base + CHUNK < len ? base + CHUNK : len;
-    const unsigned wb = base > (unsigned)HIST ? base - HIST : 0;
-    const unsigned wn = cend - wb, a0 = base - wb, clen = cend - base;
+    // the window reaches HIST bytes back; for the first chunk of a context-
+    // takeover message those are the connection's earlier plaintext (hist
+    // bytes before the message)
+    const unsigned back = base + hist < (unsigned)HIST ? base + hist : (unsigned)HIST;
+    const int wb = (int)base - (int)back;
+    const unsigned wn = cend - base + back, a0 = back, clen = cend - base;
     const bool stored_only = P.L.parser == P_STORED;
 
     Win W;
@@ -1022,7 +1027,9 @@ deflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
     Prof pf;
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
         const uint32_t len = in_len[i];
-        if (HIST == 0 ? len > CHUNK : len <= CHUNK) continue;
+        // context takeover needs the history window: all its messages take the HIST kernel
+        if (HIST == 0 ? (len > CHUNK || P.hist_len) : (len <= CHUNK && !P.hist_len)) continue;
+        const unsigned hist = P.hist_len ? (P.hist_len[i] < (unsigned)HIST ? P.hist_len[i] : (unsigned)HIST) : 0u;
         MsgOut o;
         o.dst = out + out_off[i];
         o.cap = out_cap[i];
@@ -1032,7 +1039,7 @@ deflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
         o.overflow = false;
         o.key = P.mask_key ? P.mask_key[i] : 0u;
         const uint8_t* msg = in + in_off[i];
-        for (uint32_t base = 0; base < len && !o.overflow; base += CHUNK) deflate_chunk<HIST>(S, msg, base, len, P, o, pf);
+        for (uint32_t base = 0; base < len && !o.overflow; base += CHUNK) deflate_chunk<HIST>(S, msg, base, len, hist, P, o, pf);
         // Flush::sync's empty stored block header (000) + pad; 00 00 FF FF stripped
         const unsigned tb = o.cbits + 3 > 8 ? 2u : 1u;
         if (!o.overflow && o.opos + tb > o.cap) o.overflow = true;
@@ -1076,8 +1083,8 @@ int launch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, ui
 namespace {
 int deflate_impl(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n, uint8_t* out,
                  const uint64_t* out_off, const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
-                 uint32_t* out_bits, const uint32_t* mask_key, int level, int window_bits, int strategy,
-                 hipStream_t stream)
+                 uint32_t* out_bits, const uint32_t* mask_key, const uint32_t* hist_len, int level, int window_bits,
+                 int strategy, hipStream_t stream)
 {
     bpmd::dfl::Params P;
     P.L = lz::level_params(level);
@@ -1086,6 +1093,7 @@ int deflate_impl(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_l
     P.max_dist = wsize - lz::LOOKAHEAD_MIN;
     P.out_bits = out_bits;
     P.mask_key = mask_key;
+    P.hist_len = hist_len;
     P.chain = lz::gpu_chain(level, true);
     int e = launch<0>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, P, stream);
     if (e) return e;
@@ -1099,8 +1107,8 @@ extern "C" int bpmd_internal_deflate_bits(const uint8_t* in, const uint64_t* in_
                                           uint32_t* out_len, int32_t* status, uint32_t* out_bits, int level,
                                           int window_bits, int strategy, hipStream_t stream)
 {
-    return deflate_impl(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, out_bits, nullptr, level,
-                        window_bits, strategy, stream);
+    return deflate_impl(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, out_bits, nullptr, nullptr,
+                        level, window_bits, strategy, stream);
 }
 
 extern "C" int bpmd_internal_deflate_keyed(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
@@ -1108,8 +1116,18 @@ extern "C" int bpmd_internal_deflate_keyed(const uint8_t* in, const uint64_t* in
                                            uint32_t* out_len, int32_t* status, int level, int window_bits,
                                            int strategy, const uint32_t* mask_key, hipStream_t stream)
 {
-    return deflate_impl(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, nullptr, mask_key, level,
-                        window_bits, strategy, stream);
+    return deflate_impl(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, nullptr, mask_key, nullptr,
+                        level, window_bits, strategy, stream);
+}
+
+extern "C" int bpmd_internal_deflate_takeover(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                              uint32_t n, uint8_t* out, const uint64_t* out_off,
+                                              const uint32_t* out_cap, uint32_t* out_len, int32_t* status, int level,
+                                              int window_bits, int strategy, const uint32_t* hist_len,
+                                              hipStream_t stream)
+{
+    return deflate_impl(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, nullptr, nullptr, hist_len,
+                        level, window_bits, strategy, stream);
 }
 
 extern "C" int bpmd_internal_deflate(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n,

@@ -837,6 +837,50 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
                 }
             }
         }
+#ifdef BPMD_P1_BRANCHLESS
+#pragma unroll
+        for (int kc = 0; kc < KCL; ++kc) {
+            if (st != S_PASS1 || st0 != S_PASS1) break;
+            // CODELENS (inflate_stream.ipp:264-327) with the outcomes as selects
+            refill();
+            const int32_t avail = tb + (int32_t)nb;
+            const uint32_t c7 = __builtin_bitreverse32((uint32_t)bb) >> 25;
+            const Sym yc = canon_decode<7>(tc.Q, c7);
+            const uint32_t L = cl_empty ? 1u : yc.L;
+            const uint32_t csym = cl_empty ? 0u : (uint32_t)T[O_CLS + (yc.idx < 19 ? yc.idx : 0u)];
+            const bool rpt = csym >= 16;
+            const uint32_t xb = csym == 16 ? 2u : csym == 17 ? 3u : csym == 18 ? 7u : 0u;
+            const uint32_t x = (uint32_t)(bb >> L) & lowmask(xb);
+            const uint32_t used = L + xb;
+            const uint32_t rep = csym == 16 ? 3u + x : csym == 17 ? 3u + x : csym == 18 ? 11u + x : 1u;
+            const uint32_t val = csym == 16 ? prev : (rpt ? 0u : csym);
+            const bool starve = avail < (int32_t)tc.root || (rpt && avail < (int32_t)used);
+            const bool bad = !starve && rpt && ((csym == 16 && have == 0) || have + rep > want);
+            const bool ok = !starve && !bad;
+            result = bad ? ST_INVALID_BIT_LENGTH_REPEAT : result;
+            st = ok ? st : S_DONE;
+            drop(ok ? used : 0u);
+            const bool wr = ok && val != 0;   // then rep <= 6
+            const uint32_t a = have, rw = wr ? rep : 0u, b = have + rw;
+            const uint64_t pat = ((uint64_t)val * 0x1111111111111111ull) & ((1ull << (4 * rw)) - 1);
+            const uint64_t v = pat << ((a & 7) * 4);
+            uint32_t* nw = (uint32_t*)(T + O_NIB) + (a >> 3);
+            __hip_atomic_fetch_or(nw, (uint32_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_or(nw + 1, (uint32_t)(v >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const uint32_t e_l = b < nlen ? b : nlen;
+            const uint32_t nl = e_l > a ? e_l - a : 0u;
+            const uint32_t e_o = b < 256 ? b : 256u;
+            const uint32_t nlo = e_o > a ? e_o - a : 0u;
+            const uint32_t s_d = a > nlen ? a : nlen;
+            const uint32_t nd = b > s_d ? b - s_d : 0u;
+            __hip_atomic_fetch_add(H + val, nl | (nlo << 10) | (nd << 20), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+            eob_seen = eob_seen || (wr && a <= 256 && 256 < b);
+            prev = ok ? val : prev;
+            have += ok ? rep : 0u;
+            st = (ok && have == want) ? S_BUILD : st;
+        }
+#else
 #pragma unroll
         for (int kc = 0; kc < KCL; ++kc) {
             if (st != S_PASS1 || st0 != S_PASS1) break;
@@ -909,6 +953,7 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
                     }
                 }
         }
+#endif
         if (st == S_BUILD) {
             if (!eob_seen) {
                 result = ST_MISSING_EOB;
@@ -977,10 +1022,18 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
                 for (uint32_t k = 0; k < 8; ++k) {
                     const uint32_t i = have + h8 + k;
                     const uint32_t l = (w >> (4 * k)) & 15u;
+#ifdef BPMD_P2_BRANCHLESS
+                    // one store per symbol, no branch: unused placements land on
+                    // a spare byte past the code-length symbols
+                    const bool use = l && i < want, lit = i < nlen;
+                    const uint32_t at = !use ? O_CLS + 31u : lit ? O_LIT + (olds[k] & 0xffffu) : O_DST + (olds[k] >> 16);
+                    T[at] = (uint8_t)(lit ? i : i - nlen);
+#else
                     if (l && i < want) {
                         if (i < nlen) T[O_LIT + (olds[k] & 0xffffu)] = (uint8_t)i;
                         else T[O_DST + (olds[k] >> 16)] = (uint8_t)(i - nlen);
                     }
+#endif
                 }
             }
             have += KNIB;

@@ -68,6 +68,8 @@ def lib():
         L.bpmd_write_batch.argtypes = [ctypes.POINTER(_Cfg), vp, vp, vp, vp, u32, vp, vp, vp, vp, vp, vp]
         L.bpmd_inflate_takeover_batch.argtypes = [ctypes.POINTER(_Cfg), vp, vp, vp, vp, u32, vp, vp, vp, vp, vp, vp]
         L.bpmd_slide_batch.argtypes = [vp, vp, vp, vp, u32, vp]
+        L.bpmd_deflate_takeover_batch.argtypes = [ctypes.POINTER(_Cfg), vp, vp, vp, vp, u32, vp, vp, vp, vp, vp, vp]
+        L.bpmd_deflate_takeover_batch.restype = ctypes.c_int
         L.bpmd_batcher_create.argtypes = [ctypes.POINTER(_Cfg), ctypes.c_int, u32, ctypes.c_size_t, ctypes.c_size_t,
                                           u32, ctypes.POINTER(vp)]
         L.bpmd_batcher_submit.argtypes = [vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t, vp, vp]
@@ -455,3 +457,60 @@ class Batcher:
             self.close()
         except Exception:
             pass
+
+
+class TakeoverDeflater:
+    """Send side of context-takeover connections: Beast's deflater keeps its
+    window across messages unless no_context_takeover was negotiated
+    (impl_base.hpp:156-166).  Each connection's plaintext accumulates in a
+    device buffer; message k is placed right after the connection's earlier
+    plaintext, whose last 4 KiB its matches may reach into.  Payloads decode
+    with any inflater that keeps its window (TakeoverInflater, Beast's)."""
+
+    HIST = 4096
+
+    def __init__(self, n_conn: int, level: int = 6, window_bits: int = 15, mem_level: int = 4,
+                 max_msg: int = 1 << 16, device="cuda"):
+        self.cfg = _Cfg(level, window_bits, mem_level, 0, 0)
+        self.max_msg = max_msg
+        self.slot = (2 * self.HIST + max_msg + 15) // 16 * 16
+        self.buf = torch.zeros(n_conn * self.slot + 16, dtype=torch.uint8, device=device)
+        self.base = torch.arange(n_conn, dtype=torch.int64, device=device) * self.slot
+        self.pos = torch.zeros(n_conn, dtype=torch.int64, device=device)
+
+    def deflate(self, src: Batch, conn=None, stream=None) -> Result:
+        L = lib()
+        dev = self.buf.device
+        n = src.n
+        conn = torch.arange(n, device=dev) if conn is None else torch.as_tensor(conn, device=dev).long()
+        lens = src.len.to(torch.int64)
+        if n and int(lens.max().item()) > self.max_msg:
+            raise BpmdError("message exceeds max_msg")
+        full = self.pos[conn] + lens > self.slot
+        if n and bool(full.any()):
+            idx = conn[full]
+            keep = torch.minimum(self.pos[idx], torch.tensor(self.HIST, device=dev))
+            p32, k32, b64 = self.pos[idx].to(torch.int32), keep.to(torch.int32), self.base[idx].contiguous()
+            _check(L.bpmd_slide_batch(_ptr(self.buf), _ptr(b64), _ptr(p32), _ptr(k32), int(idx.numel()),
+                                      _stream_handle(stream)), "bpmd_slide_batch")
+            self.pos[idx] = keep
+        pos = self.pos[conn]
+        in_off = (self.base[conn] + pos).contiguous()
+        total = int(lens.sum().item()) if n else 0
+        if total:   # place the messages after each connection's plaintext
+            start = torch.cumsum(lens, 0) - lens
+            j = torch.arange(total, device=dev) - torch.repeat_interleave(start, lens)
+            self.buf[torch.repeat_interleave(in_off, lens) + j] = src.data[torch.repeat_interleave(src.off, lens) + j]
+        hist = torch.minimum(pos, torch.tensor(self.HIST, device=dev)).to(torch.int32)
+        cap = (lens + (lens + 7) // 8 + (lens + 63) // 64 + 11).to(torch.int32)
+        out_off = slot_offsets(cap)
+        out = torch.empty(int(out_off[-1].item() + cap[-1].item()) + 16 if n else 16, dtype=torch.uint8,
+                          device=dev)
+        out_len = torch.empty(n, dtype=torch.int32, device=dev)
+        status = torch.empty(n, dtype=torch.int32, device=dev)
+        in_len = src.len.to(torch.int32).contiguous()
+        _check(L.bpmd_deflate_takeover_batch(ctypes.byref(self.cfg), _ptr(self.buf), _ptr(in_off), _ptr(in_len),
+                                             _ptr(hist), n, _ptr(out), _ptr(out_off), _ptr(cap), _ptr(out_len),
+                                             _ptr(status), _stream_handle(stream)), "bpmd_deflate_takeover_batch")
+        self.pos[conn] = pos + lens
+        return Result(Batch(out, out_off, out_len), cap, status)

@@ -197,6 +197,18 @@ int bpmd_inflate_takeover_batch(const bpmd_cfg* cfg, const uint8_t* d_in, const 
                                 uint8_t* d_out, const uint64_t* d_out_off, const uint32_t* d_out_cap,
                                 uint32_t* d_out_len, int32_t* d_status, void* stream);
 
+/* Send side of the same connections: Beast's deflater is not reset between
+ * messages (do_context_takeover_write resets only under no_context_takeover,
+ * impl_base.hpp:156-166), so its payloads may copy from earlier messages.
+ * Message i's bytes at d_in + d_in_off[i] are preceded in d_in by
+ * d_hist_len[i] bytes of that connection's earlier plaintext; matches reach
+ * up to 4 KiB back into them (this engine's history window; the stream stays
+ * valid for any windowBits >= 12 inflater).  Otherwise as bpmd_deflate_batch. */
+int bpmd_deflate_takeover_batch(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_off,
+                                const uint32_t* d_in_len, const uint32_t* d_hist_len, uint32_t n_msgs,
+                                uint8_t* d_out, const uint64_t* d_out_off, const uint32_t* d_out_cap,
+                                uint32_t* d_out_len, int32_t* d_status, void* stream);
+
 /* ---------------------------------------------------------------------
  * Cross-connection micro-batcher.  Beast runs one codec
  * call per message inside each connection's async operation

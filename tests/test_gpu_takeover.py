@@ -71,3 +71,37 @@ def test_distance_past_the_window_is_invalid():
         for c in range(64):
             if r == 0 or all(expect[c][k][0] == 0 for k in range(r)):
                 assert st[c] == expect[c][r][0], (r, c, st[c], expect[c][r][0])
+
+
+def test_takeover_deflate_round_trips_and_shrinks():
+    """GPU deflate with context takeover: every connection's payload stream
+    inflates (oracle, window kept) back to its messages, and reaching into
+    earlier messages makes the payloads smaller than independent ones."""
+    import torch
+    from beast_amd import pmd
+    rng = random.Random(31)
+    n_conn, rounds = 150, 5
+    msgs = []
+    for c in range(n_conn):
+        msgs.append([bytes(synth.make_batch("json", [rng.choice([1, 300, 2000, 4096, 6000])], seed=c * 7 + r)[0])
+                     for r in range(rounds)])
+    td = pmd.TakeoverDeflater(n_conn, level=6, max_msg=6000)
+    pls = [[None] * rounds for _ in range(n_conn)]
+    took = plain = 0
+    for r in range(rounds):
+        src = pmd.Batch.from_host([msgs[c][r] for c in range(n_conn)])
+        res = td.deflate(src)
+        ind = pmd.deflate_batch(src, level=6)
+        torch.cuda.synchronize()
+        assert res.status.cpu().tolist() == [0] * n_conn
+        outs = res.out.to_host()
+        for c in range(n_conn):
+            pls[c][r] = outs[c]
+        if r:
+            took += sum(len(o) for o in outs)
+            plain += sum(ind.out.len.cpu().tolist())
+    for c in range(n_conn):
+        got = O.pmd_inflate_stream(pls[c], cap=6000)
+        assert [g[0] for g in got] == [0] * rounds, c
+        assert [g[1] for g in got] == msgs[c], c
+    assert took < plain, (took, plain)
