@@ -250,7 +250,12 @@ typedef uint2 uint2_u __attribute__((aligned(1)));
 __device__ __forceinline__ void store_bounded(uint8_t* o, uint32_t dst, uint32_t sz, uint32_t lim, uint4 w)
 {
     if (dst + sz <= lim) {
+#ifdef BPMD_NT_OUT
+        typedef unsigned v4s_ __attribute__((ext_vector_type(4), aligned(1)));
+        if (sz == 16) __builtin_nontemporal_store((v4s_){w.x, w.y, w.z, w.w}, (v4s_*)(o + dst));
+#else
         if (sz == 16) *(uint4_u*)(o + dst) = w;
+#endif
         else *(uint2_u*)(o + dst) = make_uint2(w.x, w.y);
         return;
     }
@@ -395,6 +400,15 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
     bool cst = false, cst_pat = false;
     uint32_t cdst = 0, csz = 0, cpd = 1, csh = 0;
     uint4 cw = make_uint4(0, 0, 0, 0);
+#ifndef BPMD_NO_C32
+#define BPMD_C32
+#endif
+#ifdef BPMD_C32
+    uint4 cw2 = cw;   // second half of a 32-byte chunk
+#endif
+#ifdef BPMD_C64
+    uint4 cw3 = cw, cw4 = cw;
+#endif
     // byte stores decided by the previous compute section (literal or stored-block bytes)
     uint32_t bcnt = 0, bdst = 0, bval = 0;
 
@@ -410,6 +424,7 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
         LP_CNT(5, __builtin_amdgcn_ballot_w64(crem != 0) != 0);
         LP_CNT(6, __builtin_amdgcn_ballot_w64(st != S_DATA && st != S_DONE) != 0);
         LP_CNT(7, __builtin_popcountll(__builtin_amdgcn_ballot_w64(st != S_DATA && st != S_DONE)));
+        LP_CNT(12, __builtin_popcountll(__builtin_amdgcn_ballot_w64(crem != 0)));
         LP_CNT(13, __builtin_amdgcn_ballot_w64(st == S_PASS1) != 0);
         LP_CNT(14, __builtin_amdgcn_ballot_w64(st == S_PASS2) != 0);
         LP_LAP(15);
@@ -446,7 +461,22 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
                 w = make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0, 0);
             }
 #ifndef BPMD_EXP_NOSTORE
-            store_bounded(o, cdst, csz, cap, w);
+#ifdef BPMD_C32
+#ifdef BPMD_C64
+            if (csz == 64) {
+                store_bounded(o, cdst, 16, cap, w);
+                store_bounded(o, cdst + 16, 16, cap, cw2);
+                store_bounded(o, cdst + 32, 16, cap, cw3);
+                store_bounded(o, cdst + 48, 16, cap, cw4);
+            } else
+#endif
+            if (csz == 32) {
+                // the chunk's used bytes pass cdst + 16, so both halves start inside the slot
+                store_bounded(o, cdst, 16, cap, w);
+                store_bounded(o, cdst + 16, 16, cap, cw2);
+            } else
+#endif
+                store_bounded(o, cdst, csz, cap, w);
 #endif
             cst = false;
             cst_pat = false;
@@ -465,22 +495,49 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
         if (nx_used) {
             const uint32_t b0 = blk * 16, E = (s + n + 3) & ~3u;
             sg_ld = b0 < E;
+#ifdef BPMD_NT_IN
+            if (sg_ld) {
+                typedef unsigned v4a_ __attribute__((ext_vector_type(4)));
+                const v4a_ t_ = __builtin_nontemporal_load((const v4a_*)(A + b0 - 4 * in_shift(b0, E)));
+                sg = make_uint4(t_.x, t_.y, t_.z, t_.w);
+            }
+#else
             if (sg_ld) sg = *(const uint4*)(A + b0 - 4 * in_shift(b0, E));
+#endif
             sg_bi = blk++;
             nx_used = false;
         }
         LP_LAP(9);
         if (crem) {
+#ifdef BPMD_C32
+            // 32 bytes per iteration when the source lies a whole 32 back
+#ifdef BPMD_C64
+            const uint32_t C = (cdist >= 64 && crem > 48) ? 64u : (cdist >= 32 && crem > 16) ? 32u : cdist >= 16 ? 16u : 8u;
+#else
+            const uint32_t C = (cdist >= 32 && crem > 16) ? 32u : cdist >= 16 ? 16u : 8u;
+#endif
+#else
             const uint32_t C = cdist >= 16 ? 16u : 8u;
+#endif
             bool ld = false;
             int32_t src = 0;   // < 0: in the window before the slot
             if (cdist < 8) {
                 const uint32_t adv0 = 8 - 8 % cdist;
                 const uint32_t adv = adv0 < crem ? adv0 : crem;
                 if (cpat_st == 2) {
-                    store_bounded(o, cq, 8, cap, make_uint4((uint32_t)cpat, (uint32_t)(cpat >> 32), 0, 0));
+                    const uint4 pw = make_uint4((uint32_t)cpat, (uint32_t)(cpat >> 32), 0, 0);
+                    store_bounded(o, cq, 8, cap, pw);
                     cq += adv;
                     crem -= adv;
+#ifdef BPMD_PAT2
+                    // adv0 is a whole number of periods: the same 8 bytes continue the run
+                    if (crem) {
+                        const uint32_t adv2 = adv0 < crem ? adv0 : crem;
+                        store_bounded(o, cq, 8, cap, pw);
+                        cq += adv2;
+                        crem -= adv2;
+                    }
+#endif
                 } else if (cpat_st == 0) {
                     // the cdist bytes before cq, read as 8 bytes that never
                     // start before the slot
@@ -512,7 +569,24 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
 #ifdef BPMD_EXP_NOHLOAD
                 cw = make_uint4(src, src + 1, src + 2, src + 3);   // timing experiment only
 #else
+#ifdef BPMD_NT_HIST
+                {
+                    typedef unsigned v4u_ __attribute__((ext_vector_type(4), aligned(1)));
+                    const v4u_ t_ = __builtin_nontemporal_load((const v4u_*)(o + src));
+                    cw = make_uint4(t_.x, t_.y, t_.z, t_.w);
+                }
+#else
                 cw = *(const uint4_u*)(o + src);
+#endif
+#ifdef BPMD_C32
+                if (C >= 32) cw2 = *(const uint4_u*)(o + src + 16);
+#ifdef BPMD_C64
+                if (C == 64) {
+                    cw3 = *(const uint4_u*)(o + src + 32);
+                    cw4 = *(const uint4_u*)(o + src + 48);
+                }
+#endif
+#endif
 #endif
                 cst = true;
             }
