@@ -67,8 +67,15 @@ static_assert(LPW >= 1 && LPW <= 64, "lanes per wave");
 #endif
 constexpr int KLIT = BPMD_KLIT;   // symbols decoded per iteration when literals lead
 static_assert(KLIT >= 1 && KLIT <= 4, "literal bytes are queued in one 32-bit word");
-constexpr int KCL = 4;            // code-length symbols per iteration (pass 1)
-constexpr int KNIB = 16;          // code lengths placed per iteration (pass 2)
+#ifndef BPMD_KCL
+#define BPMD_KCL 4
+#endif
+#ifndef BPMD_KNIB
+#define BPMD_KNIB 16
+#endif
+constexpr int KCL = BPMD_KCL;     // code-length symbols per iteration (pass 1; <= 8: 8 x 14 bits fit the reader)
+constexpr int KNIB = BPMD_KNIB;   // code lengths placed per iteration (pass 2; a multiple of 8)
+static_assert(KCL >= 1 && KCL <= 8 && KNIB % 8 == 0 && KNIB <= 32, "header batching");
 
 enum : uint32_t { S_TYPE, S_DATA, S_SHDR, S_SCOPY, S_DYN, S_PASS1, S_BUILD, S_PASS2, S_DONE };
 
@@ -424,7 +431,6 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
         LP_CNT(5, __builtin_amdgcn_ballot_w64(crem != 0) != 0);
         LP_CNT(6, __builtin_amdgcn_ballot_w64(st != S_DATA && st != S_DONE) != 0);
         LP_CNT(7, __builtin_popcountll(__builtin_amdgcn_ballot_w64(st != S_DATA && st != S_DONE)));
-        LP_CNT(12, __builtin_popcountll(__builtin_amdgcn_ballot_w64(crem != 0)));
         LP_CNT(13, __builtin_amdgcn_ballot_w64(st == S_PASS1) != 0);
         LP_CNT(14, __builtin_amdgcn_ballot_w64(st == S_PASS2) != 0);
         LP_LAP(15);
@@ -598,6 +604,7 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
         // from the next one, except that a block header may run in the same
         // iteration as its type bits (<= 74 bits together).
         const uint32_t st0 = st;
+        LP_CNT(12, __builtin_popcountll(__builtin_amdgcn_ballot_w64(st == S_DATA && crem == 0)));
         // ================================================ decode a token
         if (st == S_DATA && crem == 0) {
             // Up to KLIT symbols per iteration: while there is room for them

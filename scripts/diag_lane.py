@@ -19,7 +19,7 @@ from beast_amd import pmd, synth  # noqa: E402
 
 NAMES = {0: "wave cycles", 1: "iterations", 2: "lanes alive/iter", 3: "iters w/ decode", 4: "lanes decoding/iter",
          5: "iters w/ copy", 6: "iters w/ header", 7: "lanes in header/iter", 8: "cyc A decode", 9: "cyc B store",
-         10: "cyc C+D headers", 11: "cyc E copy", 12: "lanes copying/iter", 13: "iters w/ pass1", 14: "iters w/ pass2", 15: "cyc loop top"}
+         10: "cyc C+D headers", 11: "cyc E copy", 12: "lanes decoding after copy issue", 13: "iters w/ pass1", 14: "iters w/ pass2", 15: "cyc loop top"}
 
 
 def main():
