@@ -240,6 +240,40 @@ int bpmd_batcher_flush(bpmd_batcher* b);
 /* Completes everything queued, then frees the batcher. */
 void bpmd_batcher_destroy(bpmd_batcher* b);
 
+/* ---------------------------------------------------------------------
+ * permessage-deflate negotiation (wire format only), for
+ * a facade that owns the handshake: the Sec-WebSocket-Extensions logic of
+ * websocket/detail/pmd_extension.hpp/.ipp.  Host code, no device use.
+ * ------------------------------------------------------------------- */
+/* detail::pmd_offer (pmd_extension.hpp:27-42) */
+typedef struct bpmd_pmd_offer {
+    int accept;
+    int server_max_window_bits;      /* 0 absent, or 8..15 (-1 present without value when writing) */
+    int client_max_window_bits;      /* -1 present without value, 0 absent, or 8..15 */
+    int server_no_context_takeover;
+    int client_no_context_takeover;
+} bpmd_pmd_offer;
+/* websocket::permessage_deflate (option.hpp:34-67); the codec fields
+ * (compLevel, memLevel, msg_size_threshold) live in bpmd_cfg */
+typedef struct bpmd_pmd_options {
+    int server_enable, client_enable;
+    int server_max_window_bits, client_max_window_bits;
+    int server_no_context_takeover, client_no_context_takeover;
+} bpmd_pmd_options;
+/* pmd_read (pmd_extension.ipp:45-166): the first permessage-deflate offer of
+ * a Sec-WebSocket-Extensions value; offer->accept = 0 when it must be declined */
+int bpmd_pmd_read(const char* ext, size_t n, bpmd_pmd_offer* offer);
+/* pmd_write (pmd_extension.ipp:168-208): the header value of an offer into
+ * out (NUL-terminated); returns its length */
+int bpmd_pmd_write(const bpmd_pmd_offer* offer, char* out, size_t cap);
+/* pmd_negotiate (pmd_extension.hpp:95-111, .ipp:210-290): the server's
+ * configuration and response value for a client offer (empty when declined);
+ * returns the response length */
+int bpmd_pmd_negotiate(const bpmd_pmd_options* o, const bpmd_pmd_offer* offer, bpmd_pmd_offer* config, char* out,
+                       size_t cap);
+/* pmd_normalize (pmd_extension.ipp:292-305) */
+void bpmd_pmd_normalize(bpmd_pmd_offer* offer);
+
 /* Window maintenance for the buffers above: move the d_keep[i] bytes before
  * d_pos[i] of the buffer at d_buf + d_base[i] to its front (the caller slides
  * only when d_pos[i] >= 2 * d_keep[i], so the ranges never overlap). */
