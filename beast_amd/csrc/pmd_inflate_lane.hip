@@ -72,6 +72,10 @@ static_assert(KLIT >= 1 && KLIT <= 4, "literal bytes are queued in one 32-bit wo
 #ifndef BPMD_NO_DUAL
 #define BPMD_DUAL
 #endif
+// ... with up to 3 literals between the two (114 -> 116.5 GiB/s)
+#if defined(BPMD_DUAL) && !defined(BPMD_NO_SUFFIX)
+#define BPMD_SUFFIX
+#endif
 #ifndef BPMD_KCL
 #define BPMD_KCL 4
 #endif
@@ -437,6 +441,11 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
     bool m2 = false, cst2 = false;
     uint32_t m2_dst = 0, m2_len = 0, cdst2 = 0, csz2 = 0;
     int32_t m2_src = 0;
+#ifdef BPMD_SUFFIX
+    // literals between the two matches: stored after the first match's chunk
+    // (two memory sections later), before the second's
+    uint32_t l2cnt = 0, l2dst = 0, l2val = 0, l2rcnt = 0, l2rdst = 0, l2rval = 0;
+#endif
     uint4 cw3 = cw, cw4 = cw;
 #endif
 #ifndef BPMD_NO_C32
@@ -454,7 +463,11 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
     LP_DECL;
     for (;;) {
 #ifdef BPMD_DUAL
+#ifdef BPMD_SUFFIX
+        const bool alive = st != S_DONE || crem != 0 || cst || bcnt != 0 || m2 || cst2 || l2cnt != 0 || l2rcnt != 0;
+#else
         const bool alive = st != S_DONE || crem != 0 || cst || bcnt != 0 || m2 || cst2;
+#endif
 #else
         const bool alive = st != S_DONE || crem != 0 || cst || bcnt != 0;
 #endif
@@ -524,6 +537,14 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
             cst_pat = false;
         }
 #ifdef BPMD_DUAL
+#ifdef BPMD_SUFFIX
+        if (l2rcnt) {
+#pragma unroll
+            for (uint32_t j = 0; j < 3; ++j)
+                if (j < l2rcnt) o[l2rdst + j] = (uint8_t)(l2rval >> (8 * j));
+            l2rcnt = 0;
+        }
+#endif
         if (cst2) {
             store_bounded(o, cdst2, 16, cap, cw3);
             if (csz2 == 32) store_bounded(o, cdst2 + 16, 16, cap, cw4);
@@ -641,6 +662,14 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
             }
         }
 #ifdef BPMD_DUAL
+#ifdef BPMD_SUFFIX
+        if (l2cnt) {   // one section later they are stored, after the first chunk
+            l2rcnt = l2cnt;
+            l2rdst = l2dst;
+            l2rval = l2val;
+            l2cnt = 0;
+        }
+#endif
         if (m2) {
             cw3 = *(const uint4_u*)(o + m2_src);
             if (m2_len > 16) cw4 = *(const uint4_u*)(o + m2_src + 16);
@@ -784,8 +813,30 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
                         // chunk and the second reads only bytes before the first
                         // (so neither waits for the other); its bits are taken only
                         // if it qualifies.  The reader must hold 48 more bits.
-                        const uint32_t held = nb + 32u * qn + (nx_used ? 0u : 128u);
                         const bool one1 = (dist >= 32 && len <= 32) || (dist >= 16 && len <= 16);
+                        uint32_t gap = 0;   // literals taken between the two matches
+#ifdef BPMD_SUFFIX
+                        if (is_match && st == S_DATA && olen == len && one1) {
+                            l2val = 0;
+#pragma unroll
+                            for (int k = 0; k < 3; ++k) {
+                                const uint32_t hk = nb + 32u * qn + (nx_used ? 0u : 128u);
+                                if (!(hk >= 128 && tb + (int32_t)nb >= 63 && pos < cap && gap == (uint32_t)k)) break;
+                                refill();
+                                const uint64_t wk = nb >= 64 ? bb : (bb | ((uint64_t)q.x << nb));
+                                const Sym yk = canon_decode<15>(tl.Q, rev15(wk));
+                                const uint32_t sk = (uint32_t)T[O_LIT + yk.idx] + (yk.idx >= LE[yk.L] ? 256u : 0u);
+                                if (yk.inval || sk >= 256) break;
+                                drop_x(yk.L);
+                                l2val |= sk << (8 * gap);
+                                l2dst = gap ? l2dst : pos;
+                                ++gap;
+                                ++pos;
+                            }
+                            l2cnt = gap;
+                        }
+#endif
+                        const uint32_t held = nb + 32u * qn + (nx_used ? 0u : 128u);
                         if (is_match && st == S_DATA && olen == len && one1 && held >= 80 &&
                             tb + (int32_t)nb >= 48) {
                             refill();   // nb >= 33: with q.x, a 64-bit window
@@ -806,7 +857,7 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
                             dist2 += (uint32_t)(w2d >> yd2.L) & lowmask(xd2);
                             const uint32_t tot2 = u2 + yd2.L + xd2;
                             const uint32_t c2 = len2 <= 16 ? 16u : 32u;   // its one chunk
-                            if (len_ok && !yd2.inval && dsym2 < 30 && len2 <= 32 && dist2 >= len + c2 &&
+                            if (len_ok && !yd2.inval && dsym2 < 30 && len2 <= 32 && dist2 >= len + gap + c2 &&
                                 dist2 <= pos + hist && pos + len2 <= cap && (int32_t)tot2 <= tb + (int32_t)nb) {
                                 drop_x(tot2);
                                 m2 = true;
