@@ -1,0 +1,108 @@
+"""GPU parity on the shapes of BASELINE.json configs C4 and C5,
+at sizes the oracle finishes in seconds.
+
+C4: Zipf message sizes 256 B - 64 KiB (synth.zipf_sizes, P(r) ∝ r^-1.1,
+size = 256·r), JSON-like text, L6 / memLevel 4.  C5: 64 KiB low-compressibility
+binary messages at deflate levels 1 and 6.
+
+Inflate: payloads made by the oracle (byte-identical to Beast's deflate) are
+inflated on both GPU kernels; output, lengths and statuses must equal the
+oracle's inflate (= the original messages).  Deflate: GPU payloads must inflate
+back byte for byte through the oracle (Beast's inflate) and the GPU inflater,
+stay within deflate_upper_bound, and stay within SIZE_TOLERANCE of Beast's
+compressed size at the same level.
+"""
+import numpy as np
+import pytest
+
+from beast_amd import synth
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+SIZE_TOLERANCE = 1.10   # Σ GPU payload bytes / Σ Beast payload bytes, same level
+
+
+def _c4(n=8192):
+    lens = synth.zipf_sizes(n, 0x5EED0004)
+    return synth.make_batch("json", lens, seed=0x5EED0004)
+
+
+def _c5(n=512):
+    lens = np.full(n, 65536, dtype=np.uint32)
+    return synth.make_batch("binary", lens, seed=0x5EED0005)
+
+
+def _gpu_inflate(comp, coff, clen, caps, kernel):
+    import torch
+    from beast_amd import pmd
+    assert pmd.lib().bpmd_set_inflate_kernel(kernel) == 0
+    try:
+        src = pmd.Batch.from_arrays(comp, coff.astype(np.int64), clen.astype(np.int32))
+        res = pmd.inflate_batch(src, torch.tensor(caps.astype(np.int32)))
+        torch.cuda.synchronize()
+        return res.status.cpu().numpy(), res.out
+    finally:
+        pmd.lib().bpmd_set_inflate_kernel(0)
+
+
+def _equal_to_messages(out, data, off, lens):
+    import torch
+    got_len = out.len.cpu().numpy()
+    assert (got_len == lens).all(), np.nonzero(got_len != lens)[0][:8]
+    # gather the GPU slots into one contiguous buffer and compare on the device
+    idx = torch.cat([torch.arange(int(o), int(o) + int(n), device=out.data.device)
+                     for o, n in zip(out.off.cpu().numpy(), lens)])
+    want = torch.from_numpy(data[: int(lens.astype(np.uint64).sum())]).to(out.data.device)
+    assert torch.equal(out.data[idx], want)
+
+
+@pytest.mark.parametrize("kernel", [1, 2], ids=["lane", "wave"])
+@pytest.mark.parametrize("cfg", ["c4", "c5_l1", "c5_l6"])
+def test_inflate_of_beast_payloads(cfg, kernel):
+    data, off, lens = _c4() if cfg == "c4" else _c5()
+    level = {"c4": 6, "c5_l1": 1, "c5_l6": 6}[cfg]
+    comp, coff, clen, cst = O.deflate_batch(data, off, lens, level=level, wbits=15, mem_level=4,
+                                            threads=16)
+    assert (cst == 0).all()
+    st, out = _gpu_inflate(comp, coff, clen, lens, kernel)
+    assert int((st != 0).sum()) == 0, np.nonzero(st)[0][:8]
+    _equal_to_messages(out, data, off, lens)
+    # one byte short of each message: need_buffers, exactly as the oracle reports
+    short = np.maximum(lens.astype(np.int64) - 1, 0).astype(np.uint32)
+    st2, _ = _gpu_inflate(comp, coff, clen, short, kernel)
+    _, _, _, est = O.inflate_batch(comp, coff, clen, short, threads=16)
+    assert (st2 == est).all(), np.nonzero(st2 != est)[0][:8]
+
+
+@pytest.mark.parametrize("cfg", ["c4", "c5_l1", "c5_l6"])
+def test_deflate_roundtrip_and_size(cfg):
+    import torch
+    from beast_amd import pmd
+    data, off, lens = _c4() if cfg == "c4" else _c5()
+    level = {"c4": 6, "c5_l1": 1, "c5_l6": 6}[cfg]
+    src = pmd.Batch.from_arrays(data, off.astype(np.int64), lens.astype(np.int32))
+    d = pmd.deflate_batch(src, level=level, mem_level=4)
+    torch.cuda.synchronize()
+    assert int((d.status != 0).sum()) == 0
+    plen = d.out.len.cpu().numpy().astype(np.uint64)
+    ub = np.array([O.upper_bound(int(x)) for x in lens], dtype=np.uint64)
+    assert (plen <= ub).all()
+    # Beast's inflate (oracle) of the GPU payloads gives the messages back
+    comp = d.out.data.cpu().numpy()
+    poff = d.out.off.cpu().numpy().astype(np.uint64)
+    out, ooff, olen, ost = O.inflate_batch(comp, poff, plen.astype(np.uint32), lens, threads=16)
+    assert (ost == 0).all() and (olen == lens).all()
+    for i in range(len(lens)):
+        a, b = int(ooff[i]), int(off[i])
+        assert np.array_equal(out[a:a + int(lens[i])], data[b:b + int(lens[i])]), i
+    # and so does the GPU inflater
+    r = pmd.inflate_batch(pmd.Batch(d.out.data, d.out.off, d.out.len),
+                          torch.tensor(lens.astype(np.int32)))
+    torch.cuda.synchronize()
+    assert int((r.status != 0).sum()) == 0
+    _equal_to_messages(r.out, data, off, lens)
+    # compressed size against Beast's at the same level
+    _, _, clen, _ = O.deflate_batch(data, off, lens, level=level, wbits=15, mem_level=4, threads=16)
+    ours, beast = int(plen.sum()), int(clen.astype(np.uint64).sum())
+    assert ours <= SIZE_TOLERANCE * beast, (ours, beast, ours / beast)
