@@ -49,18 +49,21 @@ LZ_HD Level level_params(int level)
     }
 }
 
-// Chain limit the GPU encoder uses: the level table's, capped at 32 for
-// messages of one 4 KiB chunk (measured on the C3 corpus: +1.5 % size vs the
-// table's 128 at level 6, still within 0.4 % of Beast's output; larger
-// messages keep the table value because their 4 KiB history already costs
-// ratio).
+// Chain limit the GPU encoder uses: the level table's, capped at
+// BPMD_CHAIN_CAP for messages of one 4 KiB chunk (C3 corpus at level 6: cap 4
+// costs +5.6 % size against Beast) and at
+// BPMD_CHAIN_CAP_MULTI (0 = the table's value) for longer messages.
 #ifndef BPMD_CHAIN_CAP
 #define BPMD_CHAIN_CAP 4
+#endif
+#ifndef BPMD_CHAIN_CAP_MULTI
+#define BPMD_CHAIN_CAP_MULTI 0
 #endif
 LZ_HD unsigned gpu_chain(int level, bool single_chunk)
 {
     const unsigned c = level_params(level).chain;
-    return single_chunk && c > BPMD_CHAIN_CAP ? (unsigned)BPMD_CHAIN_CAP : c;
+    const unsigned cap = single_chunk ? (unsigned)BPMD_CHAIN_CAP : (unsigned)BPMD_CHAIN_CAP_MULTI;
+    return cap && c > cap ? cap : c;
 }
 
 LZ_HD int ilog2(uint32_t v) { return 31 - __builtin_clz(v); }

@@ -75,10 +75,10 @@ template <int HIST>
 struct alignas(16) DefLds {
     static constexpr unsigned W = HIST + CHUNK;
     // window bytes at byte offset `ws`; output bit buffer after the parse.  The
-    // single-chunk layout has no slack (ws = 0): 20480 B per wave, 8 waves per
-    // CU; reads past the data land in `a` and are clamped by the lookahead, and
+    // window has no slack (ws = 0): single-chunk 20480 B per wave, 8 waves per
+    // CU, history kernel 32768 B, 5 waves per CU; reads past the data land in `a` and are clamped by the lookahead, and
     // the bit buffer's last words spill into lf[] only after lf is dead.
-    uint32_t win[(W + (HIST ? 128 : 0)) / 4];
+    uint32_t win[W / 4];
     union {
         uint16_t prev[W < 4096 ? 4096 : W];
         HuffLds h;
@@ -90,6 +90,7 @@ struct alignas(16) DefLds {
 };
 
 static_assert(sizeof(DefLds<0>) == 160 * 1024 / 8, "single-chunk deflate LDS: 8 waves per CU");
+static_assert(sizeof(DefLds<4096>) == 32768, "history deflate LDS: 5 waves per CU");
 static_assert(offsetof(HuffLds, lf) == 0, "bit buffer spill lands in lf[] (dead while packing)");
 
 struct Params {
@@ -158,26 +159,21 @@ __device__ __forceinline__ unsigned load_window(DefLds<HIST>& S, const uint8_t* 
     const uint4* g = (const uint4*)(a - s);
     const unsigned units = (s + nbytes + 15) >> 4;
     uint4* l = (uint4*)S.win;
-    if constexpr (HIST != 0) {
-        for (unsigned u = lane_id(); u < units; u += WAVE) l[u] = g[u];
-        return s;
-    } else {
-        // aligned 16-byte loads (never past the aligned unit holding the last
-        // byte), shifted down by s bytes so the window starts at LDS byte 0
-        const unsigned q = s >> 2, r = (s & 3) * 8;
-        for (unsigned u = lane_id(); u < ((nbytes + 15) >> 4); u += WAVE) {
-            const uint4 x = g[u];
-            const uint4 y = u + 1 < units ? g[u + 1] : make_uint4(0, 0, 0, 0);
-            const uint32_t d0 = q == 0 ? x.x : q == 1 ? x.y : q == 2 ? x.z : x.w;
-            const uint32_t d1 = q == 0 ? x.y : q == 1 ? x.z : q == 2 ? x.w : y.x;
-            const uint32_t d2 = q == 0 ? x.z : q == 1 ? x.w : q == 2 ? y.x : y.y;
-            const uint32_t d3 = q == 0 ? x.w : q == 1 ? y.x : q == 2 ? y.y : y.z;
-            const uint32_t d4 = q == 0 ? y.x : q == 1 ? y.y : q == 2 ? y.z : y.w;
-            l[u] = make_uint4(__builtin_amdgcn_alignbit(d1, d0, r), __builtin_amdgcn_alignbit(d2, d1, r),
-                              __builtin_amdgcn_alignbit(d3, d2, r), __builtin_amdgcn_alignbit(d4, d3, r));
-        }
-        return 0;
+    // aligned 16-byte loads (never past the aligned unit holding the last
+    // byte), shifted down by s bytes so the window starts at LDS byte 0
+    const unsigned q = s >> 2, r = (s & 3) * 8;
+    for (unsigned u = lane_id(); u < ((nbytes + 15) >> 4); u += WAVE) {
+        const uint4 x = g[u];
+        const uint4 y = u + 1 < units ? g[u + 1] : make_uint4(0, 0, 0, 0);
+        const uint32_t d0 = q == 0 ? x.x : q == 1 ? x.y : q == 2 ? x.z : x.w;
+        const uint32_t d1 = q == 0 ? x.y : q == 1 ? x.z : q == 2 ? x.w : y.x;
+        const uint32_t d2 = q == 0 ? x.z : q == 1 ? x.w : q == 2 ? y.x : y.y;
+        const uint32_t d3 = q == 0 ? x.w : q == 1 ? y.x : q == 2 ? y.y : y.z;
+        const uint32_t d4 = q == 0 ? y.x : q == 1 ? y.y : q == 2 ? y.z : y.w;
+        l[u] = make_uint4(__builtin_amdgcn_alignbit(d1, d0, r), __builtin_amdgcn_alignbit(d2, d1, r),
+                          __builtin_amdgcn_alignbit(d3, d2, r), __builtin_amdgcn_alignbit(d4, d3, r));
     }
+    return 0;
 }
 
 // ---------------------------------------------------------------- bit sink
@@ -1085,6 +1081,10 @@ deflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
 }  // namespace dfl
 }  // namespace bpmd
 
+#ifndef BPMD_HIST_WPC
+#define BPMD_HIST_WPC 4
+#endif
+
 extern "C" unsigned bpmd_diag_grid_override;   // pmd_capi.hip; 0 = size the grid by occupancy
 
 namespace {
@@ -1096,7 +1096,11 @@ int launch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, ui
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const unsigned per_cu = (160u * 1024u) / (unsigned)sizeof(bpmd::dfl::DefLds<HIST>);
-    unsigned grid = (unsigned)cus * (per_cu ? per_cu : 1u);
+    // the history kernel fits 5 waves per CU by LDS, but 5 waves on 4 SIMDs
+    // leave one SIMD shared and its waves set the end of the launch (C5:
+    // 7.0 GiB/s at 5, 10.7 at 4)
+    const unsigned cap_cu = HIST ? (unsigned)BPMD_HIST_WPC : per_cu;
+    unsigned grid = (unsigned)cus * (per_cu ? (per_cu < cap_cu ? per_cu : cap_cu) : 1u);
     if (bpmd_diag_grid_override) grid = bpmd_diag_grid_override;
     if (grid > n) grid = n;
     hipLaunchKernelGGL(bpmd::dfl::deflate_kernel<HIST>, dim3(grid), dim3(64), 0, stream, in, in_off, in_len, n, out,
