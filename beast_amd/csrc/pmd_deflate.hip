@@ -32,6 +32,8 @@
 //      dynamic, deflate_stream.ipp:1425-1518);
 //   7. bit packing: per-lane bit counts, wave prefix sum, ds_or into an LDS
 //      bit buffer, dword stores to the output slot.
+#include <atomic>
+
 #include "pmd_common.h"
 #include "wave_util.h"
 #include "lz_core.h"
@@ -101,7 +103,14 @@ struct Params {
     uint32_t* out_bits;  // optional: payload length in bits before the sync-marker tail
     const uint32_t* mask_key;   // optional: mask payload i with key i on the way out (write.hpp:679-685)
     const uint32_t* hist_len;   // optional (context takeover): plaintext bytes before message i usable as history
+    uint32_t* queue;     // optional: message counter of this launch (waves take the next message as they finish)
 };
+
+// Per-launch message counters for the history kernel's work queue: the host
+// zeroes slot k on the launch's stream and passes it in Params::queue, so
+// launches in flight on other streams use other slots.
+constexpr unsigned QUEUE_SLOTS = 4096;
+__device__ uint32_t g_queue[QUEUE_SLOTS];
 
 // Diagnostic build only (-DBPMD_PROF): per-phase wave cycles and counts.
 __device__ unsigned long long g_dprof[24];
@@ -1046,7 +1055,15 @@ deflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
     __shared__ DefLds<HIST> S;
     const unsigned lane = lane_id();
     Prof pf;
-    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    // multi-chunk messages vary from 2 to 16+ chunks: waves take them from a
+    // queue so no wave is left with a run of large ones (grid stride otherwise)
+    auto next = [&](uint32_t strided) -> uint32_t {
+        if (!P.queue) return strided;
+        uint32_t v = 0;
+        if (lane == 0) v = atomicAdd(P.queue, 1u);
+        return (uint32_t)__shfl((int)v, 0);
+    };
+    for (uint32_t i = next(blockIdx.x); i < n; i = next(i + gridDim.x)) {
         const uint32_t len = in_len[i];
         // context takeover needs the history window: all its messages take the HIST kernel
         if (HIST == 0 ? (len > CHUNK || P.hist_len) : (len <= CHUNK && !P.hist_len)) continue;
@@ -1085,7 +1102,10 @@ deflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
 #define BPMD_HIST_WPC 4
 #endif
 
-extern "C" unsigned bpmd_diag_grid_override;   // pmd_capi.hip; 0 = size the grid by occupancy
+extern "C" unsigned bpmd_diag_grid_override;
+// diagnostic: 1 = history kernel on a static grid stride (no work queue)
+extern "C" unsigned bpmd_deflate_static_grid;
+unsigned bpmd_deflate_static_grid = 0;   // pmd_capi.hip; 0 = size the grid by occupancy
 
 namespace {
 template <int HIST>
@@ -1103,8 +1123,19 @@ int launch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, ui
     unsigned grid = (unsigned)cus * (per_cu ? (per_cu < cap_cu ? per_cu : cap_cu) : 1u);
     if (bpmd_diag_grid_override) grid = bpmd_diag_grid_override;
     if (grid > n) grid = n;
+    bpmd::dfl::Params Q = P;
+    Q.queue = nullptr;
+    if (HIST && n > grid && !bpmd_deflate_static_grid) {
+        static std::atomic<unsigned> seq{0};
+        static uint32_t* base = nullptr;
+        if (!base && hipGetSymbolAddress((void**)&base, HIP_SYMBOL(bpmd::dfl::g_queue)) != hipSuccess) base = nullptr;
+        if (base) {
+            Q.queue = base + (seq.fetch_add(1u) % bpmd::dfl::QUEUE_SLOTS);
+            if (hipMemsetAsync(Q.queue, 0, sizeof(uint32_t), stream) != hipSuccess) return (int)hipGetLastError();
+        }
+    }
     hipLaunchKernelGGL(bpmd::dfl::deflate_kernel<HIST>, dim3(grid), dim3(64), 0, stream, in, in_off, in_len, n, out,
-                       out_off, out_cap, out_len, status, P);
+                       out_off, out_cap, out_len, status, Q);
     return (int)hipGetLastError();
 }
 }  // namespace

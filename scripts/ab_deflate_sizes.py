@@ -1,7 +1,9 @@
 """Times GPU deflate on the C4 (Zipf 256 B-64 KiB JSON, L6) and C5 (64 KiB binary,
 L1 and L6) shapes for library variants: median of 5 launches by HIP events on
 the current stream, GiB/s of uncompressed input, and the compressed ratio.
-VARIANTS="prev" python scripts/ab_deflate_sizes.py   (libbeast_pmd_<v>.so)"""
+VARIANTS="prev" python scripts/ab_deflate_sizes.py   (libbeast_pmd_<v>.so)
+STATIC=1 adds the product library with the history kernel on a static grid
+stride (bpmd_deflate_static_grid) instead of its work queue."""
 import ctypes
 import os
 import sys
@@ -34,6 +36,8 @@ def main():
     libs = [("default", "libbeast_pmd.so")] + [(v, f"libbeast_pmd_{v}.so")
                                                for v in os.environ.get("VARIANTS", "").split()]
     libs = [(v, ctypes.CDLL(os.path.join(ROOT, "beast_amd", f))) for v, f in libs]
+    if os.environ.get("STATIC"):
+        libs.insert(1, ("static", libs[0][1]))
     for name, level, (raw, off, ln) in workloads():
         n = len(ln)
         d_in = torch.from_numpy(raw).to(dev)
@@ -52,6 +56,8 @@ def main():
         p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
         total = int(ln.astype(np.int64).sum())
         for v, L in libs:
+            if v in ("default", "static"):
+                ctypes.c_uint.in_dll(L, "bpmd_deflate_static_grid").value = 1 if v == "static" else 0
             s = torch.cuda.current_stream().cuda_stream
             args = (ctypes.byref(cfg), p(d_in), p(d_off), p(d_len), ctypes.c_uint32(n), p(out), p(o_off), p(cap),
                     p(olen), p(st), ctypes.c_void_p(s))
