@@ -15,6 +15,16 @@ extern "C" int bpmd_internal_inflate_keyed(const uint8_t* in, const uint64_t* in
                                            uint32_t* out_len, int32_t* status, uint32_t raw, const uint32_t* mask_key,
                                            hipStream_t stream);
 
+extern "C" int bpmd_internal_inflate_keyed_split(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                                 uint32_t n, uint8_t* out, const uint64_t* out_off,
+                                                 const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
+                                                 uint32_t raw, const uint32_t* mask_key, uint32_t min_in,
+                                                 hipStream_t stream);
+extern "C" int bpmd_internal_inflate_lane_split(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                                uint32_t n, uint8_t* out, const uint64_t* out_off,
+                                                const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
+                                                uint32_t raw, const uint32_t* mask_key, const uint32_t* hist_len,
+                                                uint32_t hist_max, uint32_t max_in, hipStream_t stream);
 extern "C" int bpmd_internal_init_fixed_lane(void);
 extern "C" int bpmd_internal_inflate_lane(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                           uint32_t n, uint8_t* out, const uint64_t* out_off,
@@ -65,7 +75,7 @@ extern "C" int bpmd_set_inflate_kernel(int mode)
     return BPMD_R_OK;
 }
 
-static bool inflate_use_lane(uint32_t n)
+static int inflate_mode()
 {
     int m = g_inflate_kernel.load();
     if (m < 0) {
@@ -73,8 +83,18 @@ static bool inflate_use_lane(uint32_t n)
         m = (e && !strcmp(e, "lane")) ? 1 : (e && !strcmp(e, "wave")) ? 2 : 0;
         g_inflate_kernel.store(m);
     }
-    if (m) return m == 1;
-    return n >= 2048;
+    return m;
+}
+
+// Automatic choice, per message: a lane-kernel wave lasts as long as its
+// longest message and a batch of few messages leaves most lanes of the chip
+// idle, so payloads longer than the split (compressed bytes; several 4 KiB
+// chunks of output) go to the wave kernel and only batches of >= 2048
+// messages use lanes at all.  BPMD_INFLATE_SPLIT overrides the split.
+static uint32_t inflate_split()
+{
+    const char* e = getenv("BPMD_INFLATE_SPLIT");
+    return e ? (uint32_t)strtoul(e, nullptr, 10) : 4096u;
 }
 
 extern "C" int bpmd_init(void)
@@ -115,11 +135,19 @@ int inflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
     int r = bpmd_init();
     if (r) return r;
     const uint32_t raw = (cfg->flags & BPMD_F_RAW) ? 1u : 0u;
-    int e = (hist || inflate_use_lane(n_msgs))
-                ? bpmd_internal_inflate_lane(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
-                                             d_status, raw, key, hist, 1u << cfg->window_bits, (hipStream_t)stream)
-                : bpmd_internal_inflate_keyed(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap,
-                                              d_out_len, d_status, raw, key, (hipStream_t)stream);
+    const hipStream_t s = (hipStream_t)stream;
+    const int m = inflate_mode();
+    // lane-kernel share: everything (hist / forced lane), nothing (forced wave /
+    // small batch), or the payloads of at most `split` bytes
+    const bool lane = hist || m == 1 || (m == 0 && n_msgs >= 2048);
+    const uint32_t split = (hist || m != 0) ? 0u : inflate_split();
+    int e = 0;
+    if (lane)
+        e = bpmd_internal_inflate_lane_split(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
+                                             d_status, raw, key, hist, 1u << cfg->window_bits, split, s);
+    if (!e && (!lane || split))
+        e = bpmd_internal_inflate_keyed_split(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap,
+                                              d_out_len, d_status, raw, key, lane ? split : 0u, s);
     return e ? BPMD_R_HIP_ERROR : BPMD_R_OK;
 }
 

@@ -846,11 +846,13 @@ inflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
                const uint32_t* __restrict__ in_len, uint32_t n_msgs, uint8_t* __restrict__ out,
                const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
                uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t raw,
-               const uint32_t* __restrict__ mask_key)
+               const uint32_t* __restrict__ mask_key, uint32_t min_in)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     WaveLds& L = *reinterpret_cast<WaveLds*>(smem);
     for (uint32_t msg = blockIdx.x; msg < n_msgs; msg += gridDim.x) {
+        // min_in != 0: only payloads longer than min_in (the lane kernel has the rest)
+        if (min_in && in_len[msg] <= min_in) continue;
         Msg m;
         m.p = in + in_off[msg];
         m.n = in_len[msg];
@@ -878,10 +880,10 @@ inflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
 
 extern "C" unsigned bpmd_diag_grid_override;   // pmd_capi.hip; 0 = size the grid by occupancy
 
-extern "C" int bpmd_internal_inflate_keyed(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+extern "C" int bpmd_internal_inflate_keyed_split(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                            uint32_t n, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                                            uint32_t* out_len, int32_t* status, uint32_t raw, const uint32_t* mask_key,
-                                           hipStream_t stream)
+                                           uint32_t min_in, hipStream_t stream)
 {
     using namespace bpmd;
     if (n == 0) return 0;
@@ -893,8 +895,17 @@ extern "C" int bpmd_internal_inflate_keyed(const uint8_t* in, const uint64_t* in
     if (bpmd_diag_grid_override) grid = bpmd_diag_grid_override;
     if (grid > n) grid = n;
     hipLaunchKernelGGL(inflate_kernel, dim3(grid), dim3(WAVE), lds, stream, in, in_off, in_len, n, out, out_off,
-                       out_cap, out_len, status, raw, mask_key);
+                       out_cap, out_len, status, raw, mask_key, min_in);
     return (int)hipGetLastError();
+}
+
+extern "C" int bpmd_internal_inflate_keyed(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                           uint32_t n, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                                           uint32_t* out_len, int32_t* status, uint32_t raw, const uint32_t* mask_key,
+                                           hipStream_t stream)
+{
+    return bpmd_internal_inflate_keyed_split(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, raw,
+                                             mask_key, 0u, stream);
 }
 
 extern "C" int bpmd_internal_inflate(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n,

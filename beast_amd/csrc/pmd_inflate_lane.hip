@@ -303,7 +303,8 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
                     const uint32_t* __restrict__ in_len, uint32_t n_msgs, uint8_t* __restrict__ out,
                     const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
                     uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t raw,
-                    const uint32_t* __restrict__ mask_key, const uint32_t* __restrict__ hist_len, uint32_t hist_max)
+                    const uint32_t* __restrict__ mask_key, const uint32_t* __restrict__ hist_len, uint32_t hist_max,
+                    uint32_t max_in)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const unsigned lane = threadIdx.x;
@@ -312,7 +313,11 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
     uint32_t* H = (uint32_t*)(T + O_HIST);
     uint16_t* LE = (uint16_t*)(T + O_LE);
 
-    const bool valid = lane < LPW && msg < n_msgs;
+    // max_in != 0: only payloads of at most max_in bytes (the rest go to the
+    // wave kernel, see inflate_impl in pmd_capi.hip)
+    bool valid = lane < LPW && msg < n_msgs;
+    if (valid && max_in && in_len[msg] > max_in) valid = false;
+    if (__ballot(valid) == 0) return;
     const uint8_t* p = in;
     uint32_t n = 0, cap = 0;
     uint8_t* o = out;
@@ -1275,18 +1280,28 @@ inflate_lane_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__
 }  // namespace lpm
 }  // namespace bpmd
 
+extern "C" int bpmd_internal_inflate_lane_split(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                                uint32_t n, uint8_t* out, const uint64_t* out_off,
+                                                const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
+                                                uint32_t raw, const uint32_t* mask_key, const uint32_t* hist_len,
+                                                uint32_t hist_max, uint32_t max_in, hipStream_t stream)
+{
+    using namespace bpmd::lpm;
+    if (n == 0) return 0;
+    const unsigned grid = (n + LPW - 1) / LPW;
+    hipLaunchKernelGGL(inflate_lane_kernel, dim3(grid), dim3(64), LPW * STRIDE, stream, in, in_off, in_len, n, out,
+                       out_off, out_cap, out_len, status, raw, mask_key, hist_len, hist_max, max_in);
+    return (int)hipGetLastError();
+}
+
 extern "C" int bpmd_internal_inflate_lane(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                           uint32_t n, uint8_t* out, const uint64_t* out_off,
                                           const uint32_t* out_cap, uint32_t* out_len, int32_t* status, uint32_t raw,
                                           const uint32_t* mask_key, const uint32_t* hist_len, uint32_t hist_max,
                                           hipStream_t stream)
 {
-    using namespace bpmd::lpm;
-    if (n == 0) return 0;
-    const unsigned grid = (n + LPW - 1) / LPW;
-    hipLaunchKernelGGL(inflate_lane_kernel, dim3(grid), dim3(64), LPW * STRIDE, stream, in, in_off, in_len, n, out,
-                       out_off, out_cap, out_len, status, raw, mask_key, hist_len, hist_max);
-    return (int)hipGetLastError();
+    return bpmd_internal_inflate_lane_split(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, raw,
+                                            mask_key, hist_len, hist_max, 0u, stream);
 }
 
 extern "C" int bpmd_internal_init_fixed_lane(void)
