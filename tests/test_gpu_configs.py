@@ -6,7 +6,7 @@ size = 256·r), JSON-like text, L6 / memLevel 4.  C5: 64 KiB low-compressibility
 binary messages at deflate levels 1 and 6.
 
 Inflate: payloads made by the oracle (byte-identical to Beast's deflate) are
-inflated on both GPU kernels; output, lengths and statuses must equal the
+inflated on both GPU kernels and in the automatic per-message split; output, lengths and statuses must equal the
 oracle's inflate (= the original messages).  Deflate: GPU payloads must inflate
 back byte for byte through the oracle (Beast's inflate) and the GPU inflater,
 stay within deflate_upper_bound, and stay within SIZE_TOLERANCE of Beast's
@@ -57,7 +57,7 @@ def _equal_to_messages(out, data, off, lens):
     assert torch.equal(out.data[idx], want)
 
 
-@pytest.mark.parametrize("kernel", [1, 2], ids=["lane", "wave"])
+@pytest.mark.parametrize("kernel", [0, 1, 2], ids=["auto", "lane", "wave"])
 @pytest.mark.parametrize("cfg", ["c4", "c5_l1", "c5_l6"])
 def test_inflate_of_beast_payloads(cfg, kernel):
     data, off, lens = _c4() if cfg == "c4" else _c5()
