@@ -108,9 +108,12 @@ struct Params {
 
 // Per-launch message counters for the history kernel's work queue: the host
 // zeroes slot k on the launch's stream and passes it in Params::queue, so
-// launches in flight on other streams use other slots.
-constexpr unsigned QUEUE_SLOTS = 4096;
-__device__ uint32_t g_queue[QUEUE_SLOTS];
+// launches in flight on other streams use other slots.  A slot holds one
+// counter (own 128-byte line) per contiguous partition of the batch; wave w
+// takes messages from partition w % QUEUE_PARTS, so the single-chunk messages
+// it skips cost an atomic on one of 64 lines rather than all on one.
+constexpr unsigned QUEUE_SLOTS = 256, QUEUE_PARTS = 64, QUEUE_STRIDE = 32;
+__device__ uint32_t g_queue[QUEUE_SLOTS * QUEUE_PARTS * QUEUE_STRIDE];
 
 // Diagnostic build only (-DBPMD_PROF): per-phase wave cycles and counts.
 __device__ unsigned long long g_dprof[24];
@@ -1057,11 +1060,15 @@ deflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
     Prof pf;
     // multi-chunk messages vary from 2 to 16+ chunks: waves take them from a
     // queue so no wave is left with a run of large ones (grid stride otherwise)
+    const unsigned part = blockIdx.x % QUEUE_PARTS;
+    const uint32_t plo = (uint32_t)((uint64_t)n * part / QUEUE_PARTS);
+    const uint32_t phi = (uint32_t)((uint64_t)n * (part + 1) / QUEUE_PARTS);
     auto next = [&](uint32_t strided) -> uint32_t {
         if (!P.queue) return strided;
         uint32_t v = 0;
-        if (lane == 0) v = atomicAdd(P.queue, 1u);
-        return (uint32_t)__shfl((int)v, 0);
+        if (lane == 0) v = atomicAdd(P.queue + part * QUEUE_STRIDE, 1u);
+        v = (uint32_t)__shfl((int)v, 0);
+        return v < phi - plo ? plo + v : n;
     };
     for (uint32_t i = next(blockIdx.x); i < n; i = next(i + gridDim.x)) {
         const uint32_t len = in_len[i];
@@ -1125,13 +1132,15 @@ int launch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, ui
     if (grid > n) grid = n;
     bpmd::dfl::Params Q = P;
     Q.queue = nullptr;
-    if (HIST && n > grid && !bpmd_deflate_static_grid) {
+    if (HIST && n > grid && grid >= bpmd::dfl::QUEUE_PARTS && !bpmd_deflate_static_grid) {
         static std::atomic<unsigned> seq{0};
         static uint32_t* base = nullptr;
         if (!base && hipGetSymbolAddress((void**)&base, HIP_SYMBOL(bpmd::dfl::g_queue)) != hipSuccess) base = nullptr;
         if (base) {
-            Q.queue = base + (seq.fetch_add(1u) % bpmd::dfl::QUEUE_SLOTS);
-            if (hipMemsetAsync(Q.queue, 0, sizeof(uint32_t), stream) != hipSuccess) return (int)hipGetLastError();
+            constexpr unsigned words = bpmd::dfl::QUEUE_PARTS * bpmd::dfl::QUEUE_STRIDE;
+            Q.queue = base + (seq.fetch_add(1u) % bpmd::dfl::QUEUE_SLOTS) * words;
+            if (hipMemsetAsync(Q.queue, 0, words * sizeof(uint32_t), stream) != hipSuccess)
+                return (int)hipGetLastError();
         }
     }
     hipLaunchKernelGGL(bpmd::dfl::deflate_kernel<HIST>, dim3(grid), dim3(64), 0, stream, in, in_off, in_len, n, out,
