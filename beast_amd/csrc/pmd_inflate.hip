@@ -850,9 +850,15 @@ inflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     WaveLds& L = *reinterpret_cast<WaveLds*>(smem);
-    for (uint32_t msg = blockIdx.x; msg < n_msgs; msg += gridDim.x) {
-        // min_in != 0: only payloads longer than min_in (the lane kernel has the rest)
-        if (min_in && in_len[msg] <= min_in) continue;
+    // the wave's messages are blockIdx.x + k * gridDim.x; their lengths are
+    // read 64 at a time (one per lane) so skipping costs no serial loads.
+    // min_in != 0: only payloads longer than min_in (the lane kernel has the rest)
+    for (uint64_t first = blockIdx.x; first < n_msgs; first += (uint64_t)WAVE * gridDim.x) {
+    const uint64_t mine = first + (uint64_t)lane_id() * gridDim.x;
+    uint64_t todo = __ballot(mine < n_msgs && (!min_in || in_len[mine] > min_in));
+    while (todo) {
+        const uint32_t msg = (uint32_t)(first + (uint64_t)__builtin_ctzll(todo) * gridDim.x);
+        todo &= todo - 1;
         Msg m;
         m.p = in + in_off[msg];
         m.n = in_len[msg];
@@ -871,6 +877,7 @@ inflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
             status[msg] = st;
         }
         wave_sync();
+    }
     }
 }
 
