@@ -10,7 +10,10 @@ batch; `value` is that inflate rate.
 Also reported (same JSON line, key "deflate"): configs[2] ("C3"), the
 round trip of 64 Ki x 4 KiB JSON (seed 0x5EED0003) through the GPU deflater
 and back through the GPU inflater -- deflate GiB/s, round-trip GiB/s,
-compressed size vs Beast's deflate at the same level.
+compressed size vs Beast's deflate at the same level.  Key "mixed":
+configs[3] ("C4", Zipf 256 B-64 KiB JSON at L6) and configs[4] ("C5", 64 KiB
+binary at L1 and L6), 1/8 of each config per GPU, GPU deflate and GPU inflate
+rates with a byte-exact round-trip check (--no-mixed skips them).
 
 Launch:  python bench.py [--gpus N --steps K --warmup W]
 N > 1 runs under torch.distributed.run: every rank works on its own 64 Ki
@@ -40,6 +43,8 @@ N_MSGS = 1 << 16
 MSG_BYTES = 4096
 SEED_C2 = 0x5EED0002
 SEED_C3 = 0x5EED0003
+SEED_C4 = 0x5EED0004
+SEED_C5 = 0x5EED0005
 
 
 def log(*a):
@@ -176,6 +181,64 @@ class Timer:
         return wall / steps, kern_ms
 
 
+C4_MSGS_PER_GPU = 131072     # x 8 GPUs = configs[3]'s 1 M messages
+C5_MSGS_PER_GPU = 2048       # x 8 GPUs = configs[4]'s 16 Ki messages
+
+
+def mixed_legs(args, rank, world, timer, dev):
+    """configs[3] (C4: Zipf 256 B-64 KiB JSON, L6/mem4) and configs[4] (C5: 64 KiB
+    low-compressibility binary, L1 and L6), 1/8 of each config per GPU (weak
+    scaling: at 8 GPUs the job is the whole config).  GPU deflate, then GPU
+    inflate of its payloads, checked byte for byte against the messages on the
+    device.  Values are GiB/s of uncompressed bytes over all ranks."""
+    steps = max(1, min(args.steps, 3))
+    out = {"steps": steps, "unit": "GiB/s"}
+    c4_lens = synth.zipf_sizes(C4_MSGS_PER_GPU, SEED_C4, first=rank * C4_MSGS_PER_GPU)
+    legs = [("c4_l6", "json", c4_lens, SEED_C4, 6)]
+    c5_lens = np.full(C5_MSGS_PER_GPU, 65536, dtype=np.uint32)
+    legs += [("c5_l1", "binary", c5_lens, SEED_C5, 1), ("c5_l6", "binary", c5_lens, SEED_C5, 6)]
+    batches = {}
+    for name, kind, lens, seed, level in legs:
+        key = (kind, seed)
+        if key not in batches:
+            first = rank * len(lens)
+            raw, off, ln = synth.make_batch(kind, lens, seed=seed, first=first)
+            batches = {key: pmd.Batch(torch.from_numpy(raw).to(dev), torch.from_numpy(off.astype(np.int64)).to(dev),
+                                      torch.from_numpy(ln.astype(np.int32)).to(dev))}
+            del raw
+        src = batches[key]
+        total = int(lens.astype(np.int64).sum())
+        cap = torch.tensor([pmd.upper_bound(int(x)) for x in lens], dtype=torch.int32, device=dev)
+        coff = pmd.slot_offsets(cap)
+        cbuf = torch.empty(int(coff[-1].item()) + int(cap[-1].item()) + 64, dtype=torch.uint8, device=dev)
+
+        def deflate_step():
+            return pmd.deflate_batch(src, level=level, mem_level=4, out_cap=cap, out=cbuf, out_off=coff)
+
+        d = deflate_step()
+        torch.cuda.synchronize()
+        comp = pmd.Batch(cbuf, coff, d.out.len.clone())
+        rbuf = torch.empty_like(src.data)
+
+        def inflate_step():
+            return pmd.inflate_batch(comp, src.len, out=rbuf, out_off=src.off)
+
+        r = inflate_step()
+        torch.cuda.synchronize()
+        ok = (int((d.status != 0).sum()) == 0 and int((r.status != 0).sum()) == 0
+              and torch.equal(r.out.len, src.len) and torch.equal(rbuf[:total], src.data[:total]))
+        if not ok:
+            log(f"[rank {rank}] {name} ROUND-TRIP FAILURE")
+        d_step, _ = timer.run(deflate_step, steps, 1)
+        i_step, _ = timer.run(inflate_step, steps, 1)
+        out[name] = {"msgs_per_gpu": len(lens), "bytes_per_gpu": total,
+                     "deflate_value": round(total * world / (1 << 30) / d_step, 3),
+                     "inflate_value": round(total * world / (1 << 30) / i_step, 3),
+                     "ratio": round(int(d.out.len.to(torch.int64).sum()) / total, 4), "roundtrip_ok": bool(ok)}
+        del cbuf, rbuf, comp, d, r
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -185,6 +248,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-deflate", action="store_true")
     ap.add_argument("--no-frame", action="store_true")
+    ap.add_argument("--no-mixed", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -359,6 +423,10 @@ def main():
             result["deflate"]["size_vs_beast"] = round(float(gpu_len[:sample].sum()) / float(beast_len.sum()), 4)
             result["deflate"]["size_sample"] = f"first {sample} messages, Σ GPU bytes / Σ Beast bytes at L6/mem4"
         del src3, out3, rt_out, d, rr
+
+    # --------------------------------- C4 / C5 shapes (configs[3], configs[4])
+    if not args.no_mixed:
+        result["mixed"] = mixed_legs(args, rank, world, timer, dev)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
