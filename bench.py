@@ -253,12 +253,21 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    # BPMD_BENCH_BACKEND=gloo rehearses the multi-rank logic with several ranks
+    # on one GPU (RCCL refuses two ranks on one device); the driver's runs use
+    # nccl (= RCCL), one rank per GPU
+    backend = os.environ.get("BPMD_BENCH_BACKEND", "nccl")
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if backend != "nccl":
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     timer = Timer(dist)
     dev = torch.device("cuda", local)
     n = args.msgs
