@@ -90,7 +90,7 @@ static int inflate_mode()
 // longest message and a batch of few messages leaves most lanes of the chip
 // idle, so payloads longer than the split (compressed bytes; several 4 KiB
 // chunks of output) go to the wave kernel and only batches of >= 2048
-// messages use lanes at all.  BPMD_INFLATE_SPLIT overrides the split.
+// messages use lanes at all; batches of >= 32 Ki messages use lanes only.  BPMD_INFLATE_SPLIT overrides the split.
 static uint32_t inflate_split()
 {
     const char* e = getenv("BPMD_INFLATE_SPLIT");
@@ -140,7 +140,9 @@ int inflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
     // lane-kernel share: everything (hist / forced lane), nothing (forced wave /
     // small batch), or the payloads of at most `split` bytes
     const bool lane = hist || m == 1 || (m == 0 && n_msgs >= 2048);
-    const uint32_t split = (hist || m != 0) ? 0u : inflate_split();
+    // from 32 Ki messages on, the lanes fill the chip whatever the sizes: no
+    // split, and no second launch (C2 +1.6 %, C4 lane-only 23.2 vs 22.6 GiB/s)
+    const uint32_t split = (hist || m != 0 || n_msgs >= 32768) ? 0u : inflate_split();
     int e = 0;
     if (lane)
         e = bpmd_internal_inflate_lane_split(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
