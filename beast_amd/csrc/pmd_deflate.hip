@@ -34,6 +34,8 @@
 //      bit buffer, dword stores to the output slot.
 #include <atomic>
 
+#include <mutex>
+
 #include "pmd_common.h"
 #include "wave_util.h"
 #include "lz_core.h"
@@ -1133,9 +1135,20 @@ int launch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, ui
     bpmd::dfl::Params Q = P;
     Q.queue = nullptr;
     if (HIST && n > grid && grid >= bpmd::dfl::QUEUE_PARTS && !bpmd_deflate_static_grid) {
+        // g_queue is a __device__ variable: one copy, at its own address, per
+        // device.  Its QUEUE_SLOTS counter slots are handed out round-robin,
+        // so at most QUEUE_SLOTS history launches may be in flight at once
+        // (over all streams) on one device.
         static std::atomic<unsigned> seq{0};
-        static uint32_t* base = nullptr;
-        if (!base && hipGetSymbolAddress((void**)&base, HIP_SYMBOL(bpmd::dfl::g_queue)) != hipSuccess) base = nullptr;
+        static std::mutex mu;
+        static uint32_t* bases[64] = {};
+        uint32_t* base = nullptr;
+        if (dev >= 0 && dev < 64) {
+            std::lock_guard<std::mutex> lk(mu);
+            if (!bases[dev] && hipGetSymbolAddress((void**)&bases[dev], HIP_SYMBOL(bpmd::dfl::g_queue)) != hipSuccess)
+                bases[dev] = nullptr;
+            base = bases[dev];
+        }
         if (base) {
             constexpr unsigned words = bpmd::dfl::QUEUE_PARTS * bpmd::dfl::QUEUE_STRIDE;
             Q.queue = base + (seq.fetch_add(1u) % bpmd::dfl::QUEUE_SLOTS) * words;
@@ -1150,23 +1163,37 @@ int launch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, ui
 }  // namespace
 
 namespace {
+// tune: null, or deflate_stream::tune's (good_length, max_lazy, nice_length,
+// max_chain) (deflate_stream.ipp:307-317) replacing the level's table row;
+// the level still picks the parser, and the chain keeps the engine's caps
 int deflate_impl(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n, uint8_t* out,
                  const uint64_t* out_off, const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
                  uint32_t* out_bits, const uint32_t* mask_key, const uint32_t* hist_len, int level, int window_bits,
-                 int strategy, hipStream_t stream)
+                 int strategy, hipStream_t stream, const int* tune = nullptr)
 {
     bpmd::dfl::Params P;
     P.L = lz::level_params(level);
+    auto clamp16 = [](int v) { return (uint16_t)(v < 0 ? 0 : v > 65535 ? 65535 : v); };
+    if (tune) {
+        P.L.good = clamp16(tune[0]);
+        P.L.lazy = clamp16(tune[1]);
+        P.L.nice = clamp16(tune[2]);
+        P.L.chain = clamp16(tune[3]);
+    }
+    auto chain = [&](bool single) {
+        const unsigned cap = single ? (unsigned)BPMD_CHAIN_CAP : (unsigned)BPMD_CHAIN_CAP_MULTI;
+        return cap && P.L.chain > cap ? cap : (unsigned)P.L.chain;
+    };
     P.strategy = strategy;
     const unsigned wsize = 1u << window_bits;
     P.max_dist = wsize - lz::LOOKAHEAD_MIN;
     P.out_bits = out_bits;
     P.mask_key = mask_key;
     P.hist_len = hist_len;
-    P.chain = lz::gpu_chain(level, true);
+    P.chain = chain(true);
     int e = launch<0>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, P, stream);
     if (e) return e;
-    P.chain = lz::gpu_chain(level, false);
+    P.chain = chain(false);
     return launch<4096>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, P, stream);
 }
 }  // namespace
@@ -1174,10 +1201,10 @@ int deflate_impl(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_l
 extern "C" int bpmd_internal_deflate_bits(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                           uint32_t n, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                                           uint32_t* out_len, int32_t* status, uint32_t* out_bits, int level,
-                                          int window_bits, int strategy, hipStream_t stream)
+                                          int window_bits, int strategy, const int* tune, hipStream_t stream)
 {
     return deflate_impl(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, out_bits, nullptr, nullptr,
-                        level, window_bits, strategy, stream);
+                        level, window_bits, strategy, stream, tune);
 }
 
 extern "C" int bpmd_internal_deflate_keyed(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
@@ -1205,7 +1232,7 @@ extern "C" int bpmd_internal_deflate(const uint8_t* in, const uint64_t* in_off, 
                                      hipStream_t stream)
 {
     return bpmd_internal_deflate_bits(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, nullptr, level,
-                                      window_bits, strategy, stream);
+                                      window_bits, strategy, nullptr, stream);
 }
 
 extern "C" int bpmd_diag_deflate_counters(unsigned long long* out, int reset)

@@ -318,6 +318,12 @@ int bpmd_deflate_stream_reset(bpmd_stream* s);
 int bpmd_deflate_stream_write(bpmd_stream* s, bpmd_zparams* zs, int flush);
 /* deflate_stream::params(zs, level, strategy, ec) (deflate_stream.ipp:307-338) */
 int bpmd_deflate_stream_params(bpmd_stream* s, bpmd_zparams* zs, int level, int strategy);
+/* deflate_stream::tune(good_length, max_lazy, nice_length, max_chain)
+ * (deflate_stream.hpp:163-181, deflate_stream.ipp:307-317): replaces the
+ * level's good/lazy/nice/chain limits for the following writes (the GPU
+ * parser still caps the chain walk); like the reference, a
+ * tune before the stream's first write is undone by its lazy init. */
+int bpmd_deflate_stream_tune(bpmd_stream* s, int good_length, int max_lazy, int nice_length, int max_chain);
 /* deflate_stream::pending(value, bits) (deflate_stream.hpp:344-348) */
 int bpmd_deflate_stream_pending(bpmd_stream* s, unsigned* value, int* bits);
 /* deflate_stream::prime(bits, value, ec) (deflate_stream.ipp:340-355) */
@@ -328,8 +334,15 @@ int bpmd_inflate_stream_create(int window_bits, bpmd_stream** out);
 int bpmd_inflate_stream_reset(bpmd_stream* s, int window_bits);
 /* inflate_stream::clear() -- a no-op in the reference (inflate_stream.ipp:49-53) */
 int bpmd_inflate_stream_clear(bpmd_stream* s);
-/* inflate_stream::write(zs, flush, ec) (inflate_stream.ipp:74-535) */
+/* inflate_stream::write(zs, flush, ec) (inflate_stream.ipp:74-535).  A
+ * resumable decoder: each call decodes its own input (plus at most one
+ * decode round again) from the checkpoint the previous call left, with the
+ * window of the last 2^windowBits output bytes kept on the device; input is
+ * reported consumed whole (kept until decoded when avail_out runs out). */
 int bpmd_inflate_stream_write(bpmd_stream* s, bpmd_zparams* zs, int flush);
+/* Memory an inflate stream holds (host: kept input; device: window, output
+ * slot and input buffers); no reference counterpart, for bounded-memory tests. */
+int bpmd_inflate_stream_footprint(const bpmd_stream* s, size_t* host_bytes, size_t* device_bytes);
 void bpmd_stream_destroy(bpmd_stream* s);
 
 #ifdef __cplusplus

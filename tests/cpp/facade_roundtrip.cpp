@@ -1,10 +1,12 @@
 // Drop-in check of the C++ facade: the exact call sequence of
 // impl_base<true>::deflate (impl_base.hpp:85-154) and of the sync read path
 // with inflate_with_eb (read.hpp:1284-1356, impl_base.hpp:168-190), written
-// against beast_amd::zlib exactly as Beast writes it against
-// boost::beast::zlib.  Exit 0 = round trip ok; 3 = no GPU engine available.
+// against boost::beast::zlib exactly as Beast writes it, compiled against the
+// drop-in headers (include/boost/beast/zlib/).  One inflater for all messages,
+// never reset (Beast resets zi only in open_pmd, impl_base.hpp:277-309).
+// Exit 0 = round trip ok; 3 = no GPU engine available.
 #include <beast_amd/permessage_deflate.hpp>
-#include <beast_amd/zlib.hpp>
+#include <boost/beast/zlib.hpp>
 
 #include <cstdio>
 #include <cstring>
@@ -12,7 +14,7 @@
 #include <string>
 #include <vector>
 
-namespace zlib = beast_amd::zlib;
+namespace zlib = boost::beast::zlib;
 
 static std::vector<unsigned char> ws_deflate(zlib::deflate_stream& zo, const std::string& msg, std::size_t wr_buf)
 {
@@ -23,7 +25,7 @@ static std::vector<unsigned char> ws_deflate(zlib::deflate_stream& zo, const std
         zlib::z_params zs;
         zs.avail_out = out.size();
         zs.next_out = out.data();
-        std::error_code ec;
+        boost::beast::error_code ec;
         while (consumed + zs.total_in < msg.size()) {
             zs.next_in = msg.data() + consumed + zs.total_in;
             zs.avail_in = std::min<std::size_t>(1000, msg.size() - consumed - zs.total_in);
@@ -53,7 +55,7 @@ static std::string ws_inflate(zlib::inflate_stream& zi, const std::vector<unsign
     std::string out;
     std::size_t pos = 0;
     std::vector<char> buf(4096);
-    std::error_code ec;
+    boost::beast::error_code ec;
     while (pos < p.size()) {
         zlib::z_params zs;
         zs.next_in = p.data() + pos;
@@ -107,7 +109,6 @@ int main()
             auto payload = ws_deflate(zo, msg, 4096);
             zo.reset();   // do_context_takeover_write under server_no_context_takeover
             std::string back = ws_inflate(zi, payload);
-            zi.reset(15);
             if (back != msg) {
                 std::fprintf(stderr, "mismatch on message %d: %zu vs %zu bytes\n", m, back.size(), msg.size());
                 return 1;

@@ -1,7 +1,16 @@
-"""The C++ facade (include/beast_amd/*.hpp) compiles against the C ABI and
-links with libbeast_pmd.so; on a GPU the impl_base<true>-style round trip
-(tests/cpp/facade_roundtrip.cpp) passes, on a CPU-only host it reports the
-missing engine instead of falling back."""
+"""The C++ facade -- the drop-in boost::beast::zlib headers under
+include/boost/beast/zlib/ -- compiles against the C ABI and links with
+libbeast_pmd.so.  On a GPU:
+
+* tests/cpp/facade_roundtrip.cpp runs impl_base<true>'s exact deflate and
+  inflate call sequences (impl_base.hpp:85-190, read.hpp:1284-1356) through
+  one never-reset inflater;
+* tests/cpp/ws_echo.cpp is configs[0] ("C1"): a WebSocket echo over a
+  loopback socketpair, permessage-deflate on with the default context
+  takeover, 1 Ki x 1 KiB text messages, every message echoed byte-exactly.
+
+On a CPU-only host the binaries report the missing engine (exit 3) instead
+of falling back."""
 import os
 import subprocess
 
@@ -10,26 +19,47 @@ import pytest
 from beast_amd import build
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = os.path.join(ROOT, "tests", "cpp", "facade_roundtrip.cpp")
-OUT = os.path.join(ROOT, "tests", "cpp", "_build", "facade_roundtrip")
+CPP = os.path.join(ROOT, "tests", "cpp")
+BUILD = os.path.join(CPP, "_build")
 
 
-def _build():
+def _build(name):
     build.build()
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    os.makedirs(BUILD, exist_ok=True)
+    src, out = os.path.join(CPP, name + ".cpp"), os.path.join(BUILD, name)
+    if os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(src), os.path.getmtime(build.LIB)):
+        return out
     libdir = os.path.dirname(build.LIB)
-    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-I", os.path.join(ROOT, "include"), SRC, "-o", OUT,
-                    "-L", libdir, "-lbeast_pmd", f"-Wl,-rpath,{libdir}", "-L/opt/rocm/lib", "-lamdhip64",
-                    "-Wl,-rpath,/opt/rocm/lib"], check=True)
-    return OUT
+    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), src, "-o",
+                    out, "-L", libdir, "-lbeast_pmd", f"-Wl,-rpath,{libdir}", "-L/opt/rocm/lib", "-lamdhip64",
+                    "-Wl,-rpath,/opt/rocm/lib", "-lpthread"], check=True)
+    return out
 
 
-def test_facade_compiles_and_links():
-    assert os.path.exists(_build())
+@pytest.mark.parametrize("name", ["facade_roundtrip", "ws_echo"])
+def test_facade_compiles_and_links(name):
+    assert os.path.exists(_build(name))
+
+
+def test_without_gpu_engine_reports_instead_of_falling_back():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    r = subprocess.run([_build("ws_echo"), "2", "64"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 3, r.stdout + r.stderr
 
 
 @pytest.mark.gpu
 def test_facade_roundtrip_on_gpu():
-    r = subprocess.run([_build()], capture_output=True, text=True, timeout=300)
+    r = subprocess.run([_build("facade_roundtrip")], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.count("ok") == 4
+
+
+@pytest.mark.gpu
+def test_c1_loopback_echo_on_gpu():
+    """configs[0]: 1 Ki x 1 KiB text messages echoed over loopback."""
+    r = subprocess.run([_build("ws_echo"), "1024", "1024"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "echo ok: 1024 messages x 1024 B" in r.stdout, r.stdout
+    print(r.stdout)

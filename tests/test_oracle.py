@@ -85,7 +85,12 @@ def test_python_zlib_agrees_at_pmd_defaults():
         assert O.pmd_deflate(msg, lvl, 15, 4) == py[:-4]
 
 
-@pytest.mark.skipif(O.ref() is None, reason="reference zlib not built here")
+# a path check, not O.ref(): collecting this module (also under -m gpu) must
+# not map the reference's compiled zlib into the process
+_REF_SO = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref", "libzref.so")
+
+
+@pytest.mark.skipif(not os.path.exists(_REF_SO), reason="reference zlib not built here")
 def test_random_configs_against_reference_zlib():
     rng = random.Random(5)
     for _ in range(150):
