@@ -110,3 +110,49 @@ extern "C" int bpmd_diag_chain(const uint32_t* d_steps, uint32_t count, uint64_t
                        d_steps, count, d_out);
     return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// Counter calibration (bench.py roofline.traffic): reads a known byte count
+// in the access patterns of the inflate kernels so rocprofv3's FETCH_SIZE
+// can be converted to bytes for THOSE patterns (MI355X_MICROARCH.md: only
+// the coalesced 16-B-per-lane stream is calibrated there, at 1/2).
+//   mode 0  coalesced: lane i of a wave reads 16 B at base + 16 * i, the wave
+//           steps by 1 KiB (the guide's streaming case)
+//   mode 1  lane slots: lane i reads its own 4 KiB slot 16 B at a time, in
+//           order (the lane kernel's input blocks and history chunks)
+// Every byte of buf is read once; the XOR is stored so nothing is elided.
+namespace bpmd {
+__global__ void __launch_bounds__(256) diag_read_kernel(const uint4* __restrict__ buf, size_t n16, int mode,
+                                                        uint32_t* __restrict__ sink)
+{
+    const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t nthreads = (size_t)gridDim.x * blockDim.x;
+    uint32_t acc = 0;
+    if (mode == 0) {
+        for (size_t i = tid; i < n16; i += nthreads) {
+            const uint4 v = buf[i];
+            acc ^= v.x ^ v.y ^ v.z ^ v.w;
+        }
+    } else {
+        const size_t slots = n16 / 256;   // 4 KiB = 256 x 16 B
+        for (size_t s = tid; s < slots; s += nthreads)
+            for (unsigned k = 0; k < 256; ++k) {
+                const uint4 v = buf[s * 256 + k];
+                acc ^= v.x ^ v.y ^ v.z ^ v.w;
+            }
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;   // practically never: keeps the loads
+}
+}  // namespace bpmd
+
+extern "C" int bpmd_diag_read_pattern(const uint8_t* d_buf, size_t bytes, int mode, uint32_t* d_sink, void* stream)
+{
+    using namespace bpmd;
+    if (((uintptr_t)d_buf & 15) || (bytes & 4095)) return -1;
+    const size_t n16 = bytes / 16;
+    // mode 1: one lane per 4 KiB slot, as many lanes as the lane kernel runs
+    const unsigned grid = mode == 0 ? 4096u : (unsigned)((n16 / 256 + 255) / 256 < 256 ? (n16 / 256 + 255) / 256 : 256);
+    hipLaunchKernelGGL(diag_read_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint4*)d_buf, n16, mode,
+                       d_sink);
+    return (int)hipGetLastError();
+}

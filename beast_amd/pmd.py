@@ -326,6 +326,13 @@ def write_batch(src: Batch, key=None, level: int = 6, window_bits: int = 15, mem
 # ------------------------------------------------------------------------
 # Context takeover
 
+def _check_unique(conn, n):
+    """One message per connection per call: two messages of one connection
+    would share an output position and history and overwrite each other."""
+    if n and int(torch.unique(conn).numel()) != n:
+        raise BpmdError("a connection appears more than once in one batch; submit its messages in separate calls")
+
+
 class TakeoverInflater:
     """Receive side of context-takeover connections: Beast's inflater keeps its
     window across messages (impl_base.hpp:192-202; inflate_stream::clear() is a
@@ -352,6 +359,7 @@ class TakeoverInflater:
         dev = self.buf.device
         n = src.n
         conn = torch.arange(n, device=dev) if conn is None else torch.as_tensor(conn, device=dev).long()
+        _check_unique(conn, n)
         cap = torch.full((n,), out_cap, dtype=torch.int32, device=dev) if isinstance(out_cap, int) \
             else out_cap.to(device=dev, dtype=torch.int32)
         if int(cap.max().item() if n else 0) > self.max_msg:
@@ -376,7 +384,10 @@ class TakeoverInflater:
         _check(L.bpmd_inflate_takeover_batch(ctypes.byref(cfg), _ptr(src.data), _ptr(src.off), _ptr(src.len),
                                              _ptr(hist), n, _ptr(self.buf), _ptr(out_off), _ptr(cap), _ptr(out_len),
                                              _ptr(status), _stream_handle(stream)), "bpmd_inflate_takeover_batch")
-        self.pos[conn] = pos + out_len.to(torch.int64)
+        # a connection whose message failed is left where it was: its window
+        # is undefined from here on (the reference's stream goes BAD), so the
+        # caller drops it (check_stop_now fails the websocket connection)
+        self.pos[conn] = pos + torch.where(status == 0, out_len, torch.zeros_like(out_len)).to(torch.int64)
         return Result(Batch(self.buf, out_off, out_len), cap, status)
 
 
@@ -483,6 +494,7 @@ class TakeoverDeflater:
         dev = self.buf.device
         n = src.n
         conn = torch.arange(n, device=dev) if conn is None else torch.as_tensor(conn, device=dev).long()
+        _check_unique(conn, n)
         lens = src.len.to(torch.int64)
         if n and int(lens.max().item()) > self.max_msg:
             raise BpmdError("message exceeds max_msg")

@@ -11,9 +11,16 @@ Also reported (same JSON line, key "deflate"): configs[2] ("C3"), the
 round trip of 64 Ki x 4 KiB JSON (seed 0x5EED0003) through the GPU deflater
 and back through the GPU inflater -- deflate GiB/s, round-trip GiB/s,
 compressed size vs Beast's deflate at the same level.  Key "mixed":
-configs[3] ("C4", Zipf 256 B-64 KiB JSON at L6) and configs[4] ("C5", 64 KiB
-binary at L1 and L6), 1/8 of each config per GPU, GPU deflate and GPU inflate
-rates with a byte-exact round-trip check (--no-mixed skips them).
+configs[3] ("C4", 1 Mi Zipf 256 B-64 KiB JSON messages at L6/mem4) and
+configs[4] ("C5", 16 Ki x 64 KiB binary at L1 and L6): the WHOLE config's
+batch is sharded over the ranks in byte-balanced contiguous ranges
+(beast_amd/shard.py; strong scaling: at N=1 one GPU runs all of it), GPU
+deflate and GPU inflate rates with a byte-exact round-trip check (--no-mixed
+skips them).  Key "cpu_baseline": the same C2 payloads (and the C3 messages
+for deflate) on the host cores, at 1 thread and at the cores this process
+may use, by the C restatement of Beast's zlib ("port") and by the
+reference's own zlib 1.3.1 compiled from its sources (oracle/_ref, when
+present).
 
 Launch:  python bench.py [--gpus N --steps K --warmup W]
 N > 1 runs under torch.distributed.run: every rank works on its own 64 Ki
@@ -86,66 +93,102 @@ def _median3(fn):
     return sorted(times)[1]
 
 
-def cpu_inflate_baseline(comp_buf, comp_off, comp_len, raw_lens, threads, budget_s=8.0):
-    """Oracle (C restatement of Beast's zlib, byte-identical to it) inflating
-    the same payloads on the host cores; bounded sample."""
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baselines(comp_buf, comp_off, comp_len, raw_lens, raw3, off3, len3, target_s=1.0):
+    """Host-core baselines on bounded samples of the C2 payloads (inflate)
+    and C3 messages (deflate, L6/mem4/w15 + pmd framing): the C restatement
+    of Beast's zlib ("port", byte-identical to Beast at L1-9) and the
+    reference's own zlib 1.3.1 ("reference", compiled from
+    test/extern/zlib-1.3.1 by oracle/Makefile), each at 1 thread and at T
+    threads = the cores this process may use (capped at 16, the box's share
+    for one GPU).  Per measurement the sample is sized for ~target_s of CPU
+    work; median of 3, outputs preallocated (oracle.time_batch)."""
     from oracle import oracle as O
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    T = max(1, min(cores, 16))
+    out = {"cpu_model": _cpu_model(), "nproc": os.cpu_count(), "cores_available": cores, "threads": T}
     n = len(comp_len)
-    t0 = time.perf_counter()
-    k = min(n, 2048)
-    O.inflate_batch(comp_buf, comp_off[:k], comp_len[:k], raw_lens[:k], threads=1)
-    per_msg = (time.perf_counter() - t0) / k
-    sample = int(min(n, max(4096, budget_s / 4 / max(per_msg, 1e-9) * threads)))
-    t = _median3(lambda: O.inflate_batch(comp_buf, comp_off[:sample], comp_len[:sample], raw_lens[:sample],
-                                         threads=threads))
-    gib = float(raw_lens[:sample].astype(np.int64).sum()) / (1 << 30)
-    return {"value": round(gib / t, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": f"{sample} x {MSG_BYTES} B C2 payloads, oracle inflate (Beast-equivalent C restatement), "
-                      f"{threads} threads, median of 3"}
+    ub = np.full(n, pmd.upper_bound(MSG_BYTES) + 16, dtype=np.uint32)
+
+    def leg(impl, inflate, threads):
+        probe_n = min(n, 256)
+        args = (comp_buf, comp_off, comp_len, raw_lens) if inflate else (raw3, off3, len3, ub)
+        pr = O.time_batch(impl, inflate, args[0], args[1][:probe_n], args[2][:probe_n], args[3][:probe_n],
+                          threads=1, reps=1)
+        if pr is None:
+            return None
+        per_msg = max(pr[0] / probe_n, 1e-9)
+        k = int(min(n, max(probe_n, target_s / per_msg * threads)))
+        t, olen = O.time_batch(impl, inflate, args[0], args[1][:k], args[2][:k], args[3][:k], threads=threads)
+        gib = float(k * MSG_BYTES) / (1 << 30)
+        return {"value": round(gib / t, 4), "msgs": k, "seconds": round(t, 4), "out_len": olen}
+
+    for name, inflate in (("inflate", True), ("deflate", False)):
+        r = {}
+        for impl in ("port", "reference"):
+            one = leg(impl, inflate, 1)
+            many = leg(impl, inflate, T) if one else None
+            if one:
+                r[impl] = {"1_thread": one["value"], f"{T}_threads": many["value"],
+                           "sample_1": f"{one['msgs']} msgs", f"sample_{T}": f"{many['msgs']} msgs"}
+                if not inflate and impl == "port":
+                    r["_beast_len"] = many["out_len"]
+                if inflate:   # the sample decodes exactly (every message is 4096 bytes)
+                    r[impl]["exact"] = bool((one["out_len"] == MSG_BYTES).all())
+        if "port" in r and "reference" in r:
+            # calibration: per-byte time of the port relative to zlib 1.3.1 on one core
+            r["t_port_over_t_zlib_1thread"] = round(r["reference"]["1_thread"] / r["port"]["1_thread"], 3)
+        out[name] = r
+    return out
 
 
-def cpu_deflate_baseline(raw, off, lens, threads, budget_s=8.0):
-    """Oracle deflate (byte-identical to Beast: L6, memLevel 4, w15, pmd
-    framing) on a bounded sample; also returns Beast's payload bytes for the
-    sample so the GPU size ratio is measured on the same messages."""
-    from oracle import oracle as O
-    n = len(lens)
-    k = min(n, 512)
-    t0 = time.perf_counter()
-    O.deflate_batch(raw, off[:k], lens[:k], level=6, mem_level=4, threads=1)
-    per_msg = (time.perf_counter() - t0) / k
-    sample = int(min(n, max(2048, budget_s / 4 / max(per_msg, 1e-9) * threads)))
-    res = {}
-
-    def run():
-        res["r"] = O.deflate_batch(raw, off[:sample], lens[:sample], level=6, mem_level=4, threads=threads)
-    t = _median3(run)
-    gib = float(lens[:sample].astype(np.int64).sum()) / (1 << 30)
-    beast_len = res["r"][2]
-    return ({"value": round(gib / t, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-             "sample": f"{sample} x {MSG_BYTES} B C3 messages, oracle deflate L6/mem4/w15 "
-                       f"(Beast-equivalent C restatement), {threads} threads, median of 3"},
-            sample, beast_len)
+def _newest(pattern):
+    import glob
+    import re
+    files = glob.glob(os.path.join(ROOT, "profiles", pattern))
+    key = lambda f: (int(re.search(r"r(\d+)", os.path.basename(f)).group(1)), os.path.getmtime(f))  # noqa: E731
+    return max(files, key=key) if files else None
 
 
 def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3
-    PMC summary (profiles/rNN_*_pmc.csv, collected by scripts/profile.sh on
-    this exact workload).  FETCH_SIZE is doubled and both counters are
-    read in KiB, per MI355X_MICROARCH.md's gfx950 notes.  None if absent."""
+    """HBM bytes per launch of `kernel` on the C2 workload, from the newest
+    rocprofv3 PMC summary of the C2-only bench (profiles/rNN_c2_pmc.csv,
+    scripts/profile.sh) and the FETCH_SIZE calibration of the same run
+    (profiles/rNN_fetch_calib.csv: bytes per counted byte for the lane
+    kernel's per-lane 16-B reads, measured on a known 2 GiB read).  Counters
+    are in KiB.  Returns (bytes, details) or (None, None)."""
     import csv
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.csv")))
-    for f in reversed(files):
-        fetch, write = [], []
-        with open(f) as fh:
+    f = _newest("r*_c2_pmc.csv")
+    if not f:
+        return None, None
+    fetch, write = [], []
+    with open(f) as fh:
+        for r in csv.DictReader(fh):
+            if r["kernel"].split("::")[-1].split("<")[0] != kernel:
+                continue
+            (fetch if r["counter"] == "FETCH_SIZE" else write).append(float(r["value_kB"]) * 1024)
+    if not fetch or not write:
+        return None, None
+    factor, calib = 1.0, None
+    c = _newest("r*_fetch_calib.csv")
+    if c:
+        with open(c) as fh:
             for r in csv.DictReader(fh):
-                if r["kernel"].split("::")[-1] != kernel:
-                    continue
-                (fetch if r["counter"] == "FETCH_SIZE" else write).append(float(r["value_kB"]))
-        if fetch and write:
-            return int((2 * float(np.median(fetch)) + float(np.median(write))) * 1024), os.path.relpath(f, ROOT)
-    return None, None
+                if r["pattern"] == "lane_slots":
+                    factor, calib = float(r["bytes_per_counted_byte"]), os.path.relpath(c, ROOT)
+    fb, wb = float(np.median(fetch)), float(np.median(write))
+    return int(fb * factor + wb), {"source": os.path.relpath(f, ROOT), "fetch_bytes_raw": int(fb),
+                                   "write_bytes": int(wb), "fetch_factor": factor, "fetch_calibration": calib}
 
 
 class Timer:
@@ -181,34 +224,49 @@ class Timer:
         return wall / steps, kern_ms
 
 
-C4_MSGS_PER_GPU = 131072     # x 8 GPUs = configs[3]'s 1 M messages
-C5_MSGS_PER_GPU = 2048       # x 8 GPUs = configs[4]'s 16 Ki messages
+C4_MSGS = 1 << 20     # configs[3]: 1 Mi Zipf messages (the whole batch, sharded over the ranks)
+C5_MSGS = 16384       # configs[4]: 16 Ki x 64 KiB
+
+
+def shard_config(lens_all, rank, world):
+    """This rank's contiguous, byte-balanced message range of a whole config
+    batch and every rank's byte count: (start, end, bytes)."""
+    from beast_amd import shard
+    ranges = shard.byte_balanced_ranges(lens_all, world)
+    s0, e0 = ranges[rank]
+    return s0, e0, [int(np.asarray(lens_all[a:b], dtype=np.int64).sum()) for a, b in ranges]
 
 
 def mixed_legs(args, rank, world, timer, dev):
     """configs[3] (C4: Zipf 256 B-64 KiB JSON, L6/mem4) and configs[4] (C5: 64 KiB
-    low-compressibility binary, L1 and L6), 1/8 of each config per GPU (weak
-    scaling: at 8 GPUs the job is the whole config).  GPU deflate, then GPU
-    inflate of its payloads, checked byte for byte against the messages on the
-    device.  Values are GiB/s of uncompressed bytes over all ranks."""
+    low-compressibility binary, L1 and L6).  Each config is ONE global batch,
+    split over the ranks into byte-balanced contiguous message ranges
+    (shard.byte_balanced_ranges); each rank synthesizes only
+    its own range (seeded by global message index), deflates it on its GPU,
+    inflates the payloads back and checks them byte for byte on the device.
+    No payload crosses ranks.  Values are GiB/s of uncompressed bytes of the
+    whole batch over the max-over-ranks time (strong scaling)."""
     steps = max(1, min(args.steps, 3))
-    out = {"steps": steps, "unit": "GiB/s"}
-    c4_lens = synth.zipf_sizes(C4_MSGS_PER_GPU, SEED_C4, first=rank * C4_MSGS_PER_GPU)
-    legs = [("c4_l6", "json", c4_lens, SEED_C4, 6)]
-    c5_lens = np.full(C5_MSGS_PER_GPU, 65536, dtype=np.uint32)
-    legs += [("c5_l1", "binary", c5_lens, SEED_C5, 1), ("c5_l6", "binary", c5_lens, SEED_C5, 6)]
+    out = {"steps": steps, "unit": "GiB/s", "scaling": "strong"}
+    c4_all = synth.zipf_sizes(args.c4_msgs, SEED_C4)
+    c5_all = np.full(args.c5_msgs, 65536, dtype=np.uint32)
+    legs = [("c4_l6", "json", c4_all, SEED_C4, 6), ("c5_l1", "binary", c5_all, SEED_C5, 1),
+            ("c5_l6", "binary", c5_all, SEED_C5, 6)]
     batches = {}
-    for name, kind, lens, seed, level in legs:
+    for name, kind, lens_all, seed, level in legs:
+        s0, e0, per_rank = shard_config(lens_all, rank, world)
+        lens = lens_all[s0:e0]
         key = (kind, seed)
         if key not in batches:
-            first = rank * len(lens)
-            raw, off, ln = synth.make_batch(kind, lens, seed=seed, first=first)
+            raw, off, ln = synth.make_batch(kind, lens, seed=seed, first=s0)
             batches = {key: pmd.Batch(torch.from_numpy(raw).to(dev), torch.from_numpy(off.astype(np.int64)).to(dev),
                                       torch.from_numpy(ln.astype(np.int32)).to(dev))}
             del raw
         src = batches[key]
         total = int(lens.astype(np.int64).sum())
-        cap = torch.tensor([pmd.upper_bound(int(x)) for x in lens], dtype=torch.int32, device=dev)
+        total_all = int(lens_all.astype(np.int64).sum())
+        ub = lens.astype(np.int64) + (lens.astype(np.int64) + 7) // 8 + (lens.astype(np.int64) + 63) // 64 + 11
+        cap = torch.from_numpy(ub.astype(np.int32)).to(dev)
         coff = pmd.slot_offsets(cap)
         cbuf = torch.empty(int(coff[-1].item()) + int(cap[-1].item()) + 64, dtype=torch.uint8, device=dev)
 
@@ -231,10 +289,13 @@ def mixed_legs(args, rank, world, timer, dev):
             log(f"[rank {rank}] {name} ROUND-TRIP FAILURE")
         d_step, _ = timer.run(deflate_step, steps, 1)
         i_step, _ = timer.run(inflate_step, steps, 1)
-        out[name] = {"msgs_per_gpu": len(lens), "bytes_per_gpu": total,
-                     "deflate_value": round(total * world / (1 << 30) / d_step, 3),
-                     "inflate_value": round(total * world / (1 << 30) / i_step, 3),
-                     "ratio": round(int(d.out.len.to(torch.int64).sum()) / total, 4), "roundtrip_ok": bool(ok)}
+        comp_bytes = int(d.out.len.to(torch.int64).sum())
+        out[name] = {"msgs": len(lens_all), "bytes": total_all, "msgs_rank0": int(e0 - s0) if rank == 0 else None,
+                     "bytes_per_rank": per_rank,
+                     "imbalance_max_over_min": round(max(per_rank) / max(1, min(per_rank)), 4),
+                     "deflate_value": round(total_all / (1 << 30) / d_step, 3),
+                     "inflate_value": round(total_all / (1 << 30) / i_step, 3),
+                     "ratio_rank_local": round(comp_bytes / max(1, total), 4), "roundtrip_ok": bool(ok)}
         del cbuf, rbuf, comp, d, r
     return out
 
@@ -249,6 +310,8 @@ def main():
     ap.add_argument("--no-deflate", action="store_true")
     ap.add_argument("--no-frame", action="store_true")
     ap.add_argument("--no-mixed", action="store_true")
+    ap.add_argument("--c4-msgs", type=int, default=C4_MSGS, help="configs[3] batch (all ranks together)")
+    ap.add_argument("--c5-msgs", type=int, default=C5_MSGS, help="configs[4] batch (all ranks together)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -304,6 +367,7 @@ def main():
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     kname = "inflate_lane_kernel" if n >= 2048 else "inflate_kernel"   # bpmd_set_inflate_kernel(0) policy
     traffic, traffic_src = pmc_traffic(kname) if n == N_MSGS else (None, None)
+    # (traffic_src: the PMC file, its raw FETCH/WRITE bytes and the FETCH calibration used)
     result = {
         "metric": "GiB/s device-resident inflate+deflate over batched WS payloads, 1/2/4/8 GPU",
         "value": round(value, 3),
@@ -426,11 +490,19 @@ def main():
                          "kernel": "deflate_kernel", "kernel_ms": round(d_kern, 4), "alg_bytes_per_launch": dalg},
         }
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            threads = min(16, os.cpu_count() or 1)
-            cb, sample, beast_len = cpu_deflate_baseline(raw3, off3, len3, threads)
-            result["deflate"]["cpu_baseline"] = cb
-            result["deflate"]["size_vs_beast"] = round(float(gpu_len[:sample].sum()) / float(beast_len.sum()), 4)
-            result["deflate"]["size_sample"] = f"first {sample} messages, Σ GPU bytes / Σ Beast bytes at L6/mem4"
+            cpu = cpu_baselines(comp_buf, comp_off, comp_len, raw_len.astype(np.uint32), raw3, off3, len3)
+            dcpu = cpu["deflate"]
+            beast_len = dcpu.pop("_beast_len", None)
+            if beast_len is not None:
+                k = len(beast_len)
+                result["deflate"]["size_vs_beast"] = round(float(gpu_len[:k].sum()) / float(beast_len.sum()), 4)
+                result["deflate"]["size_sample"] = f"first {k} messages, Σ GPU bytes / Σ Beast bytes at L6/mem4"
+            if "port" in dcpu:
+                T = cpu["threads"]
+                result["deflate"]["cpu_baseline"] = {
+                    "value": dcpu["port"][f"{T}_threads"], "unit": "GiB/s", "cores": T, "kind": "port",
+                    "sample": f"C3 messages, {dcpu['port'][f'sample_{T}']}, L6/mem4/w15 + pmd framing",
+                    "one_thread": dcpu["port"]["1_thread"], "reference_zlib_1.3.1": dcpu.get("reference")}
         del src3, out3, rt_out, d, rr
 
     # --------------------------------- C4 / C5 shapes (configs[3], configs[4])
@@ -438,9 +510,18 @@ def main():
         result["mixed"] = mixed_legs(args, rank, world, timer, dev)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = min(16, os.cpu_count() or 1)
-        result["cpu_baseline"] = cpu_inflate_baseline(comp_buf, comp_off, comp_len, raw_len.astype(np.uint32),
-                                                      threads)
+        if args.no_deflate:
+            cpu = cpu_baselines(comp_buf, comp_off, comp_len, raw_len.astype(np.uint32), raw, raw_off, raw_len)
+        icpu = cpu["inflate"]
+        T = cpu["threads"]
+        if "port" in icpu:
+            result["cpu_baseline"] = {
+                "value": icpu["port"][f"{T}_threads"], "unit": "GiB/s", "cores": T, "kind": "port",
+                "sample": f"C2 payloads, {icpu['port'][f'sample_{T}']} x {MSG_BYTES} B, oracle inflate "
+                          f"(C restatement of Beast's zlib), {T} threads, median of 3",
+                "one_thread": icpu["port"]["1_thread"], "reference_zlib_1.3.1": icpu.get("reference"),
+                "t_port_over_t_zlib_1thread": icpu.get("t_port_over_t_zlib_1thread"),
+                "cpu_model": cpu["cpu_model"], "nproc": cpu["nproc"], "cores_available": cpu["cores_available"]}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:

@@ -93,6 +93,9 @@ def ref():
         R.zref_inflate.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_ulong, ctypes.c_void_p,
                                    ctypes.c_ulong, ctypes.POINTER(ctypes.c_int)]
         R.zref_inflate.restype = ctypes.c_long
+        vp = ctypes.c_void_p
+        R.zref_batch.argtypes = [ctypes.c_int] * 4 + [vp] * 3 + [ctypes.c_uint32] + [vp] * 4 + [ctypes.c_int]
+        R.zref_batch.restype = ctypes.c_int
         _REF = R
     return _REF
 
@@ -331,3 +334,65 @@ def pmd_inflate_stream(payloads, cap: int = 1 << 20, wbits=15):
         return res
     finally:
         L.bzo_inflate_free(z)
+
+
+def ref_batch(inflate: bool, data, off, lens, out_cap, level=6, wbits=15, mem_level=4, threads=1):
+    """The reference's zlib 1.3.1 over a batch (CPU baseline / calibration):
+    inflate = payload + 00 00 FF FF with Z_SYNC_FLUSH, deflate = pmd framing.
+    Returns (out, out_off, out_len) or None when libzref.so is absent."""
+    R = ref()
+    if R is None:
+        return None
+    n = len(lens)
+    out_cap = np.ascontiguousarray(out_cap, dtype=np.uint32)
+    out_off = np.zeros(n, dtype=np.uint64)
+    if n:
+        out_off[1:] = np.cumsum(out_cap[:-1].astype(np.uint64))
+    out = np.zeros(int(out_cap.astype(np.uint64).sum()) + 1, dtype=np.uint8)
+    out_len = np.zeros(n, dtype=np.uint32)
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    R.zref_batch(1 if inflate else 0, level, wbits, mem_level, _p(data), _p(off), _p(lens), n, _p(out),
+                 _p(out_off), _p(out_cap), _p(out_len), threads)
+    return out, out_off, out_len
+
+
+def time_batch(impl: str, inflate: bool, data, off, lens, out_cap, threads=1, reps=3, level=6, wbits=15,
+               mem_level=4):
+    """Median wall seconds of one batch call on the host cores, outputs
+    preallocated outside the timed region.  impl: "port" (this C restatement
+    of Beast's zlib) or "reference" (the reference's zlib 1.3.1, oracle/_ref).
+    Returns (seconds, out_len) or None when the implementation is absent."""
+    import time
+    n = len(lens)
+    out_cap = np.ascontiguousarray(out_cap, dtype=np.uint32)
+    out_off = np.zeros(n, dtype=np.uint64)
+    if n:
+        out_off[1:] = np.cumsum(out_cap[:-1].astype(np.uint64))
+    out = np.ones(int(out_cap.astype(np.uint64).sum()) + 1, dtype=np.uint8)   # touched: no page faults timed
+    out_len = np.zeros(n, dtype=np.uint32)
+    status = np.zeros(n, dtype=np.int32)
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    if impl == "reference":
+        R = ref()
+        if R is None:
+            return None
+        call = lambda: R.zref_batch(1 if inflate else 0, level, wbits, mem_level, _p(data), _p(off), _p(lens), n,  # noqa: E731
+                                    _p(out), _p(out_off), _p(out_cap), _p(out_len), threads)
+    elif inflate:
+        L = lib()
+        call = lambda: L.bzo_pmd_inflate_batch(wbits, 0, _p(data), _p(off), _p(lens), n, _p(out), _p(out_off),  # noqa: E731
+                                               _p(out_cap), _p(out_len), _p(status), threads)
+    else:
+        L = lib()
+        call = lambda: L.bzo_pmd_deflate_batch(level, wbits, mem_level, 0, _p(data), _p(off), _p(lens), n,  # noqa: E731
+                                               _p(out), _p(out_off), _p(out_cap), _p(out_len), _p(status), threads)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        call()
+        ts.append(time.perf_counter() - t0)
+    return sorted(ts)[len(ts) // 2], out_len.copy()

@@ -80,3 +80,50 @@ def test_two_rank_gloo_shards_and_collectives():
     assert res[0][2] == 0 and res[1][2] == len(res[0][5]) and res[0][3] == res[1][3] == len(expect)
     assert res[0][5] + res[1][5] == expect
     assert res[0][4] == res[1][4] == 2.0
+
+
+def _bench_worker(rank, world, port, q):
+    """bench.py's own partition code (shard_config + per-rank synthesis by
+    global message index) on a C4-shaped batch under gloo."""
+    import sys
+    import torch.distributed as dist
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lens_all = synth.zipf_sizes(600, bench.SEED_C4)
+    s0, e0, per_rank = bench.shard_config(lens_all, rank, world)
+    data, off, ln = synth.make_batch("json", lens_all[s0:e0], seed=bench.SEED_C4, first=s0)
+    local = [O.pmd_deflate(bytes(data[int(off[i]):int(off[i]) + int(ln[i])]), 6, 15, 4) for i in range(len(ln))]
+    start, total = shard.global_output_offsets(sum(len(x) for x in local))
+    q.put((rank, (s0, e0), per_rank, start, total, b"".join(local)))
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_runs_bench_partition():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in range(world)])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    lens_all = synth.zipf_sizes(600, bench.SEED_C4)
+    data, off, ln = synth.make_batch("json", lens_all, seed=bench.SEED_C4)
+    expect = b"".join(O.pmd_deflate(bytes(data[int(off[i]):int(off[i]) + int(ln[i])]), 6, 15, 4)
+                      for i in range(len(ln)))
+    (r0, g0, b0, st0, tot0, out0), (r1, g1, b1, st1, tot1, out1) = res
+    assert g0[0] == 0 and g0[1] == g1[0] and g1[1] == len(lens_all)
+    assert b0 == b1 and sum(b0) == int(lens_all.astype(np.int64).sum())
+    assert max(b0) - min(b0) <= 2 * int(lens_all.max())
+    assert st0 == 0 and st1 == len(out0) and tot0 == tot1 == len(expect)
+    assert out0 + out1 == expect   # per-rank synthesis by global index == the whole batch
