@@ -1,0 +1,1069 @@
+// pmd_inflate_lane2.hip -- batched raw-DEFLATE decode, one LANE per message,
+// second design: a leaner decode step for two waves per SIMD, and lanes that
+// take a new message when theirs is done.
+//
+// Each lane runs the reference's serial decoder (include/boost/beast/zlib/
+// detail/inflate_stream.ipp:74-535) on its own message; the output slot is
+// the window (history reads are plain loads of the lane's own earlier
+// stores).  Differences from the first design (pmd_inflate_lane.hip, round 1):
+//
+//  * Speculative multi-symbol decode.  The code LENGTH of a symbol comes from
+//    the canonical limit words in registers, so the bit positions of the next
+//    KLIT symbols -- assuming the earlier ones are literals -- are known
+//    before any LDS read; their KLIT symbol lookups then go out together and
+//    cost one LDS round trip instead of KLIT dependent ones.  The length /
+//    distance pair of the iteration's main token is the second round trip.
+//  * No second match per iteration: fewer registers (<= 256 VGPR+AGPR with no
+//    spills), so two waves share each SIMD: with one wave per SIMD a wave
+//    issues at most one instruction every ~4 cycles and stalls on every LDS
+//    and memory wait; with two, one wave's VALU overlaps the other's SALU,
+//    LDS and memory waits (MI355X_MICROARCH.md, issue costs).  A 64 Ki batch
+//    runs 32 messages per wave (BPMD2_LPW) to get two waves per SIMD.
+//  * Work queue: with `qctr` set, a lane whose message is done takes the next
+//    one (`order[k]`, e.g. longest first) from a per-launch counter, one
+//    atomic per wave and refill, so a batch of mixed sizes (configs[3]) keeps
+//    every lane busy until the queue is empty.
+//
+// The reference's fill rule (a step needs the bits the slow path would NEED,
+// root / sub-table index bits included, bitstream.hpp:109-121) only matters
+// within 48 bits of the end of the input; there the exact need is recomputed
+// from the canonical limits.  Output semantics per message are those of
+// pmd_inflate.hip (statuses, lengths, capacity rules).
+#include "pmd_common.h"
+
+namespace bpmd {
+namespace lp2 {
+
+// per-lane LDS layout (bytes)
+constexpr unsigned O_LIT = 0;      // u8[288]  literal/length symbols, canonical order (low 8 bits)
+constexpr unsigned O_DST = 288;    // u8[32]   distance symbols, canonical order
+constexpr unsigned O_HIST = 320;   // u32[16]  pass 1: length histogram (lit | lit<256 << 10 | dist << 20)
+                                   //          pass 2: placement cursors (lit | dist << 16)
+constexpr unsigned O_LE = 384;     // u16[16]  litend per code length
+constexpr unsigned O_CLS = 416;    // u8[20]   code-length code symbols, canonical order
+constexpr unsigned O_NIB = 448;    // u8[160]  code lengths, one nibble per symbol
+constexpr unsigned STRIDE = 624;   // 256 lanes per CU x 624 B fit the 160 KiB LDS
+
+#ifndef BPMD2_LPW
+#define BPMD2_LPW 32
+#endif
+#ifndef BPMD2_WPS
+#define BPMD2_WPS 2
+#endif
+constexpr unsigned LPW = BPMD2_LPW;   // messages per wave (lanes past LPW idle)
+static_assert(LPW >= 1 && LPW <= 64, "lanes per wave");
+constexpr int KLIT = 4;   // symbols decoded per iteration when literals lead (bytes queue in one u32)
+constexpr int KCL = 4;    // code-length symbols per iteration (pass 1; 4 x 14 bits fit the reader)
+constexpr int KNIB = 16;  // code lengths placed per iteration (pass 2; a multiple of 8)
+
+enum : uint32_t { S_TYPE, S_DATA, S_SHDR, S_SCOPY, S_DYN, S_PASS1, S_BUILD, S_PASS2, S_DONE };
+
+template <int NB>
+struct Canon {
+    uint32_t Q[NB];
+    uint32_t root;   // the reference's (clamped) root table bits
+};
+
+template <int NB>
+__device__ __forceinline__ uint32_t canon_min(const uint32_t (&Q)[NB], uint32_t c)
+{
+    const uint32_t k1 = (c + 1) << 15;
+    uint32_t m = Q[0] - k1;
+#pragma unroll
+    for (int i = 1; i + 1 < NB; i += 2) {
+        const uint32_t x = Q[i] - k1, y = Q[i + 1] - k1;
+        m = __builtin_elementwise_min(m, __builtin_elementwise_min(x, y));
+    }
+    if (NB % 2 == 0) m = __builtin_elementwise_min(m, Q[NB - 1] - k1);
+    return m;
+}
+
+struct Sym {
+    uint32_t L;     // code length
+    uint32_t idx;   // canonical index (0 when invalid)
+    bool inval;
+};
+
+template <int NB>
+__device__ __forceinline__ Sym canon_decode(const uint32_t (&Q)[NB], uint32_t c)
+{
+    const uint32_t m = canon_min<NB>(Q, c);
+    Sym r;
+    r.inval = (m >> 31) != 0;
+    const uint32_t q = m + ((c + 1) << 15);
+    r.L = (q >> 11) & 15u;
+    const int32_t below = (int32_t)(c - (q >> 15)) >> (NB - (int32_t)r.L);   // in [-count_L, -1]
+    r.idx = r.inval ? 0u : (uint32_t)((int32_t)(q & 0x7ffu) + below);
+    return r;
+}
+
+// The reference's slow path asks for the root bits, or for root + sub-table
+// index bits when the code is longer than the root: a sub-table covers one
+// root prefix and is as deep as the longest code under it, i.e. the length
+// of the last code of the prefix's range (inflate_stream.ipp:360-420, 688-709).
+template <int NB>
+__device__ __forceinline__ uint32_t canon_need(const Canon<NB>& t, const Sym& y, uint32_t c)
+{
+    if (y.inval || y.L <= t.root) return t.root;
+    const uint32_t re = c | ((1u << (NB - t.root)) - 1u);
+    return ((canon_min<NB>(t.Q, re) + ((re + 1) << 15)) >> 11) & 15u;
+}
+
+__device__ __forceinline__ uint32_t rev15(uint64_t bb) { return __builtin_bitreverse32((uint32_t)bb) >> 17; }
+__device__ __forceinline__ uint32_t lowmask(uint32_t n) { return n >= 32 ? ~0u : ((1u << n) - 1u); }
+
+// counts c[1..NB] -> canonical words; returns 0, 14 or 15 following
+// inflate_table's acceptance rules (inflate_stream.ipp:574-617).
+// type: 0 codes, 1 lens, 2 dists.  (The first canonical index of length l
+// is the running sum of c[1..l-1]; callers that need it recompute it.)
+template <int NB>
+__device__ __forceinline__ int make_canon(const uint32_t (&c)[16], uint32_t R, int type, Canon<NB>& t)
+{
+    uint32_t hi = 0, lo = 0;
+#pragma unroll
+    for (int l = NB; l >= 1; --l)
+        if (c[l]) lo = l;
+#pragma unroll
+    for (int l = 1; l <= NB; ++l)
+        if (c[l]) hi = l;
+    int left = 1;
+    bool over = false;
+#pragma unroll
+    for (int l = 1; l <= NB; ++l) {
+        left = 2 * left - (int)c[l];
+        over |= left < 0;
+    }
+    uint32_t lim = 0, cu = 0;
+#pragma unroll
+    for (int l = 1; l <= NB; ++l) {
+        cu += c[l];
+        lim += c[l] << (NB - l);
+        t.Q[l - 1] = (lim << 15) | ((uint32_t)l << 11) | cu;
+    }
+    if (hi == 0) {   // empty code: a 1-bit root of invalid slots
+        t.root = 1;
+        return 0;
+    }
+    const uint32_t r = R < hi ? R : hi;
+    t.root = r < lo ? lo : r;
+    if (over) return ST_OVER_SUBSCRIBED_LENGTH;
+    if (left > 0 && (type == 0 || hi != 1)) return ST_INCOMPLETE_LENGTH_SET;
+    return 0;
+}
+
+// Input blocks: 16 stream bytes at A + 16*bi, where the payload is
+// [s, s+n) (A = payload & ~3).  issue_block() reads only dwords holding at
+// least one payload byte -- an aligned dword lies in one page, so nothing
+// past the payload's last page is touched -- and finish_block(), run after
+// the data has arrived, turns the bytes past the payload into the
+// 00 00 FF FF tail (pmd mode) and then zeros.
+__device__ __forceinline__ uint4 issue_block(const uint8_t* A, uint32_t bi, uint32_t s, uint32_t n)
+{
+    const uint32_t b0 = bi * 16;
+    if (b0 + 16 <= s + n) return *(const uint4*)(A + b0);
+    const uint32_t* A32 = (const uint32_t*)(A + b0);
+    uint4 w = make_uint4(0, 0, 0, 0);
+    if (b0 + 4 > s && b0 < s + n) w.x = A32[0];
+    if (b0 + 8 > s && b0 + 4 < s + n) w.y = A32[1];
+    if (b0 + 12 > s && b0 + 8 < s + n) w.z = A32[2];
+    if (b0 + 16 > s && b0 + 12 < s + n) w.w = A32[3];
+    return w;
+}
+__device__ __forceinline__ uint32_t finish_dword(uint32_t d, int32_t r0, uint32_t n, uint32_t tail)
+{
+    // r0: payload index of the dword's first byte
+    const int32_t valid = (int32_t)n - r0;
+    if (valid >= 4) return d;
+    d &= valid <= 0 ? 0u : ((1u << (8 * valid)) - 1u);
+    if (tail) {
+        const int32_t t2 = (int32_t)n + 2 - r0, t3 = t2 + 1;   // FF FF of 00 00 FF FF
+        if (t2 >= 0 && t2 < 4) d |= 0xffu << (8 * t2);
+        if (t3 >= 0 && t3 < 4) d |= 0xffu << (8 * t3);
+    }
+    return d;
+}
+__device__ __forceinline__ uint4 finish_block(uint4 w, uint32_t bi, uint32_t s, uint32_t n, uint32_t tail)
+{
+    const uint32_t b0 = bi * 16;
+    if (b0 + 16 <= s + n) return w;
+    const int32_t r0 = (int32_t)b0 - (int32_t)s;
+    return make_uint4(finish_dword(w.x, r0, n, tail), finish_dword(w.y, r0 + 4, n, tail),
+                      finish_dword(w.z, r0 + 8, n, tail), finish_dword(w.w, r0 + 12, n, tail));
+}
+
+// In-loop input block bi >= 2 (b0 >= 32): one 16-byte load, clamped to end
+// at E = the end of the payload's last dword (so it never touches a page
+// past the payload), or no load at all past E.  The block's dwords are the
+// loaded ones shifted down by m; finish_in() applies that shift and the tail.
+__device__ __forceinline__ uint32_t in_shift(uint32_t b0, uint32_t E) { return b0 + 16 > E ? (b0 + 16 - E) >> 2 : 0u; }
+__device__ __forceinline__ uint4 finish_in(uint4 w, bool ld, uint32_t bi, uint32_t s, uint32_t n, uint32_t tail,
+                                           uint32_t mk)
+{
+    const uint32_t b0 = bi * 16;
+    const uint32_t E = (s + n + 3) & ~3u;
+    w = ld ? make_uint4(w.x ^ mk, w.y ^ mk, w.z ^ mk, w.w ^ mk) : make_uint4(0, 0, 0, 0);   // unmask (mk: 0 or the key)
+    const uint32_t m = ld ? in_shift(b0, E) : 0u;
+    uint4 v = w;
+    if (m == 1) v = make_uint4(w.y, w.z, w.w, 0);
+    if (m == 2) v = make_uint4(w.z, w.w, 0, 0);
+    if (m == 3) v = make_uint4(w.w, 0, 0, 0);
+    return finish_block(v, bi, s, n, tail);
+}
+
+typedef uint4 uint4_u __attribute__((aligned(1)));
+typedef uint2 uint2_u __attribute__((aligned(1)));
+
+// Reads of the lane's own earlier output (match sources) are plain loads:
+// within one wave the vector L1 is coherent with the wave's own stores
+// (AMDGPU memory model, GFX90A/GFX942: no action is needed for coherence
+// between the lanes of a wavefront).
+
+// Store the first n of the sz (8 or 16) bytes of w at o + dst, never past
+// o + lim: whole when it fits (spare bytes past n are overwritten by later
+// output), byte by byte from registers at the end of the slot.
+__device__ __forceinline__ void store_bounded(uint8_t* o, uint32_t dst, uint32_t sz, uint32_t lim, uint4 w)
+{
+    if (dst + sz <= lim) {
+        if (sz == 16) *(uint4_u*)(o + dst) = w;
+        else *(uint2_u*)(o + dst) = make_uint2(w.x, w.y);
+        return;
+    }
+    const uint32_t k = lim - dst;   // < sz
+    const uint32_t d[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j)
+        if (j < k) o[dst + j] = (uint8_t)(d[j >> 2] >> (8 * (j & 3)));
+}
+
+static __constant__ const uint8_t kClenOrder2[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+// per-launch work queue: wave-level grabs of `need` messages (<= 64)
+__device__ __forceinline__ uint32_t queue_grab(uint32_t* qctr, uint64_t need_mask)
+{
+    const uint32_t k = (uint32_t)__builtin_popcountll(need_mask);
+    const unsigned leader = (unsigned)__builtin_ctzll(need_mask);
+    uint32_t base = 0;
+    if (threadIdx.x == leader) base = atomicAdd(qctr, k);
+    return __shfl(base, (int)leader);
+}
+
+__global__ void __launch_bounds__(64, BPMD2_WPS)
+inflate_lane2_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                     const uint32_t* __restrict__ in_len, uint32_t n_msgs, uint8_t* __restrict__ out,
+                     const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
+                     uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t raw,
+                     const uint32_t* __restrict__ mask_key, const uint32_t* __restrict__ hist_len, uint32_t hist_max,
+                     uint32_t max_in, const uint32_t* __restrict__ order, uint32_t* __restrict__ qctr)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const unsigned lane = threadIdx.x;
+    uint8_t* T = smem + (lane % LPW) * STRIDE;
+    uint32_t* H = (uint32_t*)(T + O_HIST);
+    uint16_t* LE = (uint16_t*)(T + O_LE);
+    const uint32_t tail = raw ? 0u : 4u;
+    const int32_t full_status = raw ? ST_OK : ST_NEED_BUFFERS;
+    // static first assignment: slot j = blockIdx.x * LPW + lane; the queue
+    // hands out slots from gridDim.x * LPW on
+    const uint32_t first_slots = gridDim.x * LPW;
+
+    // ---- per-message state
+    uint32_t msg = 0;
+    bool valid = false;
+    const uint8_t* A = in;
+    uint32_t s = 0, n = 0, cap = 0, mk = 0, hist = 0;
+    uint8_t* o = out;
+    // bit reader: bb holds up to 64 bits; refills take 32-bit words from q
+    // (a 16-byte block, shifted down as it is used), then from nx (the next
+    // block, already in registers).  Blocks move nx <- sg <- memory only in
+    // the loop's memory section, so decoding never waits on memory.
+    uint4 q = make_uint4(0, 0, 0, 0), nx = q, sg = q;
+    uint32_t blk = 3, qn = 4, sg_bi = 2;
+    bool nx_used = false, sg_ld = false;
+    uint64_t bb = 0;
+    uint32_t nb = 0;
+    int32_t tb = 0;   // stream bits not yet moved into bb
+    uint32_t st = S_DONE;
+    int32_t result = ST_OK;
+    bool last = false;
+    uint32_t pos = 0;
+    Canon<15> tl, td;
+    Canon<7> tc;
+    // header state
+    uint32_t nlen = 0, ndist = 0, want = 0, have = 0, prev = 0;
+    bool eob_seen = false, cl_empty = false;
+    // stored block
+    uint32_t srem = 0;
+    bool sfull = false, sstarve = false;
+    // match copy: bytes left to issue, distance, next output position
+    uint32_t crem = 0, cdist = 0, cq = 0;
+    uint64_t cpat = 0;
+    uint32_t cpat_st = 0;   // dist < 8: 0 pattern not requested, 1 source bytes in flight, 2 pattern ready
+    // chunk loaded in the previous memory section, stored in the next one
+    bool cst = false, cst_pat = false;
+    uint32_t cdst = 0, csz = 0, cpd = 1, csh = 0;
+    uint4 cw = make_uint4(0, 0, 0, 0), cw2 = cw;
+    // byte stores decided by the previous compute section (literal or stored-block bytes)
+    uint32_t bcnt = 0, bdst = 0, bval = 0;
+
+    auto refill = [&]() {   // branchless: in a wave some lane nearly always needs it
+        const bool need = nb <= 32;
+        const uint64_t add = (uint64_t)q.x << (nb & 63);
+        bb |= need ? add : 0ull;
+        nb += need ? 32u : 0u;
+        tb -= need ? 32 : 0;
+        q.x = need ? q.y : q.x;
+        q.y = need ? q.z : q.y;
+        q.z = need ? q.w : q.z;
+        qn -= need ? 1u : 0u;
+        const bool sw = qn == 0;
+        q.x = sw ? nx.x : q.x;
+        q.y = sw ? nx.y : q.y;
+        q.z = sw ? nx.z : q.z;
+        q.w = sw ? nx.w : q.w;
+        qn = sw ? 4u : qn;
+        nx_used = nx_used || sw;
+    };
+    // consume t <= 60 bits of the 64-bit window bb | q.x << nb (nb >= 33)
+    auto drop_x = [&](uint32_t t) {
+        const bool over = t > nb;
+        const uint32_t r = (t - nb) & 31u;
+        const uint64_t a = bb >> (t & 63u);
+        const uint64_t b = (uint64_t)(q.x >> r);
+        bb = over ? b : a;
+        nb = over ? 32u - r : nb - t;
+        tb -= over ? 32 : 0;
+        q.x = over ? q.y : q.x;
+        q.y = over ? q.z : q.y;
+        q.z = over ? q.w : q.z;
+        qn -= over ? 1u : 0u;
+        const bool sw = qn == 0;
+        q.x = sw ? nx.x : q.x;
+        q.y = sw ? nx.y : q.y;
+        q.z = sw ? nx.z : q.z;
+        q.w = sw ? nx.w : q.w;
+        qn = sw ? 4u : qn;
+        nx_used = nx_used || sw;
+    };
+    auto drop = [&](uint32_t k) {
+        bb >>= k;
+        nb -= k;
+    };
+    // set the lane up for message m (its first two input blocks are loaded
+    // here, the third is issued into sg)
+    auto start = [&](uint32_t m) {
+        msg = m;
+        valid = true;
+        if (max_in && in_len[m] > max_in) valid = false;   // the wave kernel has it (pmd_capi.hip)
+        const uint8_t* p = in;
+        n = 0;
+        cap = 0;
+        o = out;
+        if (valid) {
+            p = in + in_off[m];
+            n = in_len[m];
+            cap = out_cap[m];
+            o = out + out_off[m];
+        }
+        s = (uint32_t)((uintptr_t)p & 3);
+        A = p - s;
+        // masked payloads (bpmd_read_batch): the dword at A + 4k holds payload
+        // bytes 4k - s .. 4k - s + 3, masked with key bytes (j - s) % 4
+        // (mask.ipp:38-59), so one rotation of the key unmasks every dword
+        mk = (valid && mask_key) ? __builtin_amdgcn_alignbit(mask_key[m], mask_key[m], 8u * ((0u - s) & 3u)) : 0u;
+        // context takeover (bpmd_inflate_takeover_batch): the hist bytes before
+        // the slot are the window Beast's inflater keeps across messages
+        hist = (valid && hist_len) ? (hist_len[m] < hist_max ? hist_len[m] : hist_max) : 0u;
+        q = make_uint4(0, 0, 0, 0);
+        nx = q;
+        if (valid) {
+            const uint4 b0w = issue_block(A, 0, s, n), b1w = issue_block(A, 1, s, n);
+            q = finish_block(make_uint4(b0w.x ^ mk, b0w.y ^ mk, b0w.z ^ mk, b0w.w ^ mk), 0, s, n, tail);
+            nx = finish_block(make_uint4(b1w.x ^ mk, b1w.y ^ mk, b1w.z ^ mk, b1w.w ^ mk), 1, s, n, tail);
+        }
+        const uint32_t E_in = (s + n + 3) & ~3u;
+        sg_ld = valid && 32 < E_in;
+        if (sg_ld) sg = *(const uint4*)(A + 32 - 4 * in_shift(32, E_in));
+        blk = 3;
+        qn = 4;
+        sg_bi = 2;
+        nx_used = false;
+        bb = 0;
+        nb = 0;
+        tb = (int32_t)(8 * (s + n + tail));
+        refill();
+        refill();
+        drop(8 * s);
+        st = valid ? (raw && n == 0 ? S_DONE : S_TYPE) : S_DONE;
+        result = (valid && raw && n == 0) ? ST_NEED_BUFFERS : ST_OK;
+        last = false;
+        pos = 0;
+#pragma unroll
+        for (int i = 0; i < 15; ++i) { tl.Q[i] = 0; td.Q[i] = 0; }
+        tl.root = 9;
+        td.root = 5;
+#pragma unroll
+        for (int i = 0; i < 7; ++i) tc.Q[i] = 0;
+        tc.root = 1;
+        srem = 0;
+        crem = 0;
+        cpat_st = 0;
+    };
+
+    {
+        const uint32_t j = blockIdx.x * LPW + lane;
+        const bool have_msg = lane < LPW && j < n_msgs;
+        if (__ballot(have_msg) == 0) return;
+        if (have_msg) start(order ? order[j] : j);
+    }
+    bool exhausted = qctr == nullptr;   // this lane will get no further message
+
+    for (;;) {
+        const bool busy = st != S_DONE || crem != 0 || cst || bcnt != 0;
+        // ---- message done: publish it, and take the next one from the queue
+        const bool finished = !busy && msg != 0xFFFFFFFFu;
+        if (finished) {
+            if (valid) {
+                out_len[msg] = pos;
+                status[msg] = result;
+            }
+            msg = 0xFFFFFFFFu;
+            valid = false;
+        }
+        if (!exhausted) {
+            const uint64_t idle = __ballot(!busy && lane < LPW);
+            // refill when a quarter of the wave waits or nothing else runs
+            if (__builtin_popcountll(idle) * 4 >= LPW || __ballot(busy) == 0) {
+                const uint32_t base = queue_grab(qctr, idle);
+                const bool mine = (idle >> lane) & 1;
+                const uint32_t k = first_slots + base +
+                                   (uint32_t)__builtin_popcountll(idle & ((1ull << lane) - 1ull));
+                if (mine) {
+                    if (k < n_msgs) start(order ? order[k] : k);
+                    else exhausted = true;
+                }
+                exhausted = __ballot(exhausted && lane < LPW) == __ballot(lane < LPW) ? true : exhausted;
+            }
+        }
+        const bool alive = st != S_DONE || crem != 0 || cst || bcnt != 0;
+        if (!__ballot(alive) && (exhausted || __ballot(!exhausted && lane < LPW) == 0)) break;
+        if (!__ballot(alive)) continue;
+
+        // ================================================ memory section
+        // Every global load of the loop is issued here and its data is only
+        // used in the next iteration's memory section, so the one wait per
+        // iteration covers loads that had a whole decode step to land.
+        // Stores go in output order (a chunk's spare tail bytes are always
+        // overwritten by a later store), and every load of earlier output
+        // is issued after the stores it reads.
+        if (nx_used) nx = finish_in(sg, sg_ld, sg_bi, s, n, tail, mk);
+        if (cst) {
+            uint4 w = cw;
+            if (cst_pat) {
+                // the cpd bytes before the match, repeated with period cpd (the
+                // match that asked for them may be finished and a new one
+                // decoded since: its distance is the request's own, cpd)
+                uint64_t v = ((uint64_t)cw.y << 32) | cw.x;
+                v >>= 8 * csh;
+                v &= (1ull << (8 * cpd)) - 1;
+                // (64-bit shifts of 64 or more wrap on the hardware: guard them)
+                if (cpd < 8) v |= v << (8 * cpd);
+                if (cpd < 4) v |= v << (16 * cpd);
+                if (cpd < 2) v |= v << (32 * cpd);
+                if (cpat_st == 1) {   // still the current match
+                    cpat = v;
+                    cpat_st = 2;
+                }
+                w = make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0, 0);
+            }
+            if (csz == 32) {
+                // the chunk's used bytes pass cdst + 16, so both halves start inside the slot
+                store_bounded(o, cdst, 16, cap, w);
+                store_bounded(o, cdst + 16, 16, cap, cw2);
+            } else {
+                store_bounded(o, cdst, csz, cap, w);
+            }
+            cst = false;
+            cst_pat = false;
+        }
+        if (bcnt) {
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j)
+                if (j < bcnt) o[bdst + j] = (uint8_t)(bval >> (8 * j));
+            bcnt = 0;
+        }
+        // ... then issue this iteration's loads
+        if (nx_used) {
+            const uint32_t b0 = blk * 16, E = (s + n + 3) & ~3u;
+            sg_ld = b0 < E;
+            if (sg_ld) sg = *(const uint4*)(A + b0 - 4 * in_shift(b0, E));
+            sg_bi = blk++;
+            nx_used = false;
+        }
+        if (crem) {
+            // 32 bytes per iteration when the source lies a whole 32 back
+            const uint32_t C = (cdist >= 32 && crem > 16) ? 32u : cdist >= 16 ? 16u : 8u;
+            bool ld = false;
+            int32_t src = 0;   // < 0: in the window before the slot
+            if (cdist < 8) {
+                const uint32_t adv0 = 8 - 8 % cdist;
+                const uint32_t adv = adv0 < crem ? adv0 : crem;
+                if (cpat_st == 2) {
+                    const uint4 pw = make_uint4((uint32_t)cpat, (uint32_t)(cpat >> 32), 0, 0);
+                    store_bounded(o, cq, 8, cap, pw);
+                    cq += adv;
+                    crem -= adv;
+                } else if (cpat_st == 0) {
+                    // the cdist bytes before cq, read as 8 bytes that never
+                    // start before the slot's window
+                    ld = true;
+                    src = max((int32_t)cq - 8, -(int32_t)hist);
+                    csh = (uint32_t)((int32_t)cq - (int32_t)cdist - src);
+                    cst_pat = true;
+                    cpd = cdist;
+                    csz = 8;
+                    cpat_st = 1;
+                    cdst = cq;
+                    cq += adv;
+                    crem -= adv;
+                }
+                // cpat_st == 1 cannot be seen here: the pattern is built in the
+                // memory section that follows the one that requested it
+            } else {
+                ld = true;
+                src = (int32_t)cq - (int32_t)cdist;
+                csz = C;
+                cdst = cq;
+                const uint32_t adv = C < crem ? C : crem;
+                cq += adv;
+                crem -= adv;
+            }
+            if (ld) {
+                // 16 (32) bytes from src: the bytes used all lie in [src, cq); the
+                // rest may run into the next slot (never stored)
+                cw = *(const uint4_u*)(o + src);
+                if (C >= 32) cw2 = *(const uint4_u*)(o + src + 16);
+                cst = true;
+            }
+        }
+
+        // Input bits per iteration stay <= 108 (the reader always holds >= 160
+        // without touching memory): a state entered during an iteration runs
+        // from the next one, except that a block header may run in the same
+        // iteration as its type bits (<= 74 bits together).
+        const uint32_t st0 = st;
+        // ================================================ decode a token
+        if (st == S_DATA && crem == 0) {
+            // Up to KLIT symbols per iteration: while there is room for them
+            // (input for KLIT - 1 literals plus a whole token, output for KLIT
+            // literals, so no event can occur among them) leading literals are
+            // taken directly; the first other symbol -- or, out of room, the
+            // first symbol of any kind -- is the iteration's main token, handled
+            // with the reference's checks below.  The KLIT code lengths come from
+            // registers, so their KLIT symbol lookups go out together.
+            refill();   // nb >= 33: with q.x, a 64-bit window
+            const uint64_t w = nb >= 64 ? bb : (bb | ((uint64_t)q.x << nb));
+            const bool multi = (tb + (int32_t)nb) >= 48 + 15 * (KLIT - 1) && pos + KLIT <= cap;
+            uint32_t kp[KLIT + 1], kc[KLIT], kL[KLIT], kx[KLIT];
+            bool kinv[KLIT];
+            kp[0] = 0;
+#pragma unroll
+            for (int k = 0; k < KLIT; ++k) {
+                kc[k] = rev15(w >> kp[k]);
+                const Sym y = canon_decode<15>(tl.Q, kc[k]);
+                kL[k] = y.L;
+                kx[k] = y.idx;
+                kinv[k] = y.inval;
+                kp[k + 1] = kp[k] + (y.inval ? 15u : y.L);
+            }
+            uint32_t kle[KLIT], ksb[KLIT];
+#pragma unroll
+            for (int k = 0; k < KLIT; ++k) {
+                kle[k] = LE[kL[k]];
+                ksb[k] = T[O_LIT + kx[k]];
+            }
+            uint32_t ks[KLIT];
+#pragma unroll
+            for (int k = 0; k < KLIT; ++k) ks[k] = ksb[k] + (kx[k] >= kle[k] ? 256u : 0u);
+            // leading literals taken directly
+            uint32_t nlit = 0, lbytes = 0;
+#pragma unroll
+            for (int k = 0; k < KLIT; ++k) {
+                const bool take = multi && nlit == (uint32_t)k && !kinv[k] && ks[k] < 256;
+                lbytes |= take ? ks[k] << (8 * k) : 0u;
+                nlit += take ? 1u : 0u;
+            }
+            const uint32_t lit_bits = nlit == 0 ? 0u : nlit == 1 ? kp[1] : nlit == 2 ? kp[2] : nlit == 3 ? kp[3] : kp[4];
+            if (nlit) {
+                bcnt = nlit;
+                bdst = pos;
+                bval = lbytes;
+                pos += nlit;
+            }
+            // the main token: symbol nlit (none when all KLIT were literals)
+            const uint32_t c15 = nlit == 0 ? kc[0] : nlit == 1 ? kc[1] : nlit == 2 ? kc[2] : kc[3];
+            const uint32_t L = nlit == 0 ? kL[0] : nlit == 1 ? kL[1] : nlit == 2 ? kL[2] : kL[3];
+            const uint32_t sym = nlit == 0 ? ks[0] : nlit == 1 ? ks[1] : nlit == 2 ? ks[2] : ks[3];
+            const bool inval =
+                (nlit == 0 ? kinv[0] : nlit == 1 ? kinv[1] : nlit == 2 ? kinv[2] : kinv[3]) || sym >= 286;
+            drop_x(lit_bits);
+            if (nlit < (uint32_t)KLIT) {
+                refill();   // nb >= 33 again: the main token's <= 48 bits are in the window
+                const uint64_t w2 = nb >= 64 ? bb : (bb | ((uint64_t)q.x << nb));
+                const int32_t avail = tb + (int32_t)nb;
+                Sym y;
+                y.L = L;
+                y.idx = 0;
+                y.inval = inval;
+                uint32_t need_l = 0;
+                if (avail < 48) need_l = canon_need<15>(tl, y, c15);
+                // length and distance are decoded for every lane (a wave nearly
+                // always holds a match): no divergent branch around them
+                const bool is_len = !inval && sym > 256;
+                const uint32_t li = is_len ? sym - 257 : 0u;
+                const uint32_t xl = (li < 8 || li == 28) ? 0u : ((li - 4) >> 2);
+                uint32_t len = li < 8 ? li + 3 : (li == 28 ? 258u : (((4u + (li & 3)) << xl) + 3));
+                len += (uint32_t)(w2 >> L) & lowmask(xl);
+                const uint32_t used = L + (is_len ? xl : 0u);
+                const uint32_t d15 = rev15(w2 >> used);
+                const Sym yd = canon_decode<15>(td.Q, d15);
+                const uint32_t Ld = yd.L;
+                const uint32_t dsym = T[O_DST + yd.idx];
+                const bool invd = yd.inval || dsym >= 30;
+                const uint32_t xd = dsym < 4 ? 0u : (dsym >> 1) - 1;
+                uint32_t dist = dsym < 4 ? dsym + 1 : (((2u + (dsym & 1)) << xd) + 1);
+                dist += (uint32_t)(w2 >> (used + Ld)) & lowmask(xd);
+                uint32_t need_d = 0;
+                if (avail < 48 && is_len) need_d = canon_need<15>(td, yd, d15);
+                bool is_match = false;
+                uint32_t ev = 0;   // 0 token, 1 eob, 2 starved, 3 error
+                int32_t err = 0;
+                uint32_t take = used;
+                if ((int32_t)need_l > avail) {
+                    ev = 2;
+                } else if (inval) {
+                    ev = 3;
+                    err = ST_INVALID_LITERAL_LENGTH;
+                } else if (sym == 256) {
+                    ev = 1;
+                } else if (sym > 256) {
+                    if ((int32_t)used > avail || (int32_t)(used + need_d) > avail) {
+                        ev = 2;
+                    } else if (invd) {
+                        ev = 3;
+                        err = ST_INVALID_DISTANCE_CODE;
+                    } else if ((int32_t)(used + Ld + xd) > avail) {
+                        ev = 2;
+                    } else {
+                        take = used + Ld + xd;
+                        is_match = true;
+                    }
+                }
+                drop_x(ev >= 2 ? 0u : take);
+                if (ev == 0) {
+                    // output checks in the reference's order (inflate_stream.ipp:475-514)
+                    if (raw && pos >= cap) {
+                        result = full_status;
+                        st = S_DONE;
+                    } else if (is_match && dist > pos + hist) {
+                        result = ST_INVALID_DISTANCE;
+                        st = S_DONE;
+                    } else if (pos >= cap) {
+                        result = full_status;
+                        st = S_DONE;
+                    } else {
+                        uint32_t olen = is_match ? len : 1u;
+                        if (pos + olen > cap) {
+                            olen = cap - pos;
+                            result = full_status;
+                            st = S_DONE;
+                        }
+                        if (is_match) {
+                            crem = olen;
+                            cdist = dist;
+                            cq = pos;
+                            cpat_st = 0;
+                        } else {
+                            bcnt = 1;
+                            bdst = pos;
+                            bval = sym;
+                        }
+                        pos += olen;
+                    }
+                } else if (ev == 1) {
+                    st = S_TYPE;
+                } else if (ev == 2) {
+                    st = S_DONE;
+                } else {
+                    result = err;
+                    st = S_DONE;
+                }
+            }
+        }
+
+        // ======================================= block headers, stored
+        if (st == S_TYPE && st0 == S_TYPE) {
+            if (last) {
+                result = ST_END_OF_STREAM;
+                st = S_DONE;
+            } else {
+                refill();
+                const int32_t avail = tb + (int32_t)nb;
+                if (avail < 3) {
+                    st = S_DONE;
+                } else {
+                    const uint32_t h = (uint32_t)bb & 7u;
+                    drop(3);
+                    last = (h & 1) != 0;
+                    const uint32_t type = h >> 1;
+                    if (type == 0) {
+                        st = S_SHDR;
+                    } else if (type == 1) {
+                        // fixed tables (inflate_stream.ipp:865-930): canonical
+                        // order is 256-279 | 0-143 280-287 | 144-255, distances 0-31
+                        uint4* dst4 = (uint4*)T;
+#pragma unroll 1
+                        for (int k = 0; k < 20; ++k) {
+                            uint32_t w4[4];
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) {
+                                const int i = 16 * k + 4 * j;
+                                const int v = i < 24 ? i : i < 168 ? i - 24 : i < 176 ? i - 144 : i < 288 ? i - 32 : i - 288;
+                                w4[j] = (uint32_t)v * 0x01010101u + 0x03020100u;
+                            }
+                            dst4[k] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+                        }
+                        LE[7] = 0;
+                        LE[8] = 168;
+                        LE[9] = 288;
+                        // make_canon of the fixed counts (7: 24, 8: 152, 9: 112; distances 5: 32)
+                        constexpr uint32_t kFixL[15] = {0x00000800u, 0x00001000u, 0x00001800u, 0x00002000u,
+                                                        0x00002800u, 0x00003000u, 0x0c003818u, 0x320040b0u,
+                                                        0x40004920u, 0x40005120u, 0x40005920u, 0x40006120u,
+                                                        0x40006920u, 0x40007120u, 0x40007920u};
+                        constexpr uint32_t kFixD[15] = {0x00000800u, 0x00001000u, 0x00001800u, 0x00002000u,
+                                                        0x40002820u, 0x40003020u, 0x40003820u, 0x40004020u,
+                                                        0x40004820u, 0x40005020u, 0x40005820u, 0x40006020u,
+                                                        0x40006820u, 0x40007020u, 0x40007820u};
+#pragma unroll
+                        for (int i = 0; i < 15; ++i) {
+                            tl.Q[i] = kFixL[i];
+                            td.Q[i] = kFixD[i];
+                        }
+                        tl.root = 9;
+                        td.root = 5;
+                        st = S_DATA;
+                    } else if (type == 2) {
+                        st = S_DYN;
+                    } else {
+                        result = ST_INVALID_BLOCK_TYPE;
+                        st = S_DONE;
+                    }
+                }
+            }
+        }
+        if (st == S_SHDR) {
+            // STORED (inflate_stream.ipp:184-204)
+            refill();
+            int32_t avail = tb + (int32_t)nb;
+            drop((uint32_t)avail & 7u);
+            avail &= ~7;
+            refill();
+            if (avail < 32) {
+                st = S_DONE;
+            } else {
+                const uint32_t v = (uint32_t)bb & 0xffffu, nv = (uint32_t)(bb >> 16) & 0xffffu;
+                if (v != (nv ^ 0xffffu)) {
+                    result = ST_INVALID_STORED_LENGTH;
+                    st = S_DONE;
+                } else {
+                    drop(32);
+                    avail -= 32;
+                    const uint32_t have_b = (uint32_t)avail >> 3;
+                    uint32_t nc = v < have_b ? v : have_b;
+                    sfull = false;
+                    if (pos + nc > cap) {
+                        nc = cap - pos;
+                        sfull = true;
+                    }
+                    sstarve = nc < v;
+                    srem = nc;
+                    st = S_SCOPY;
+                }
+            }
+        }
+        if (st == S_SCOPY) {
+            // COPY (inflate_stream.ipp:206-220): up to 4 bytes per iteration,
+            // stored by the next memory section (after any literals this
+            // iteration already queued before its end of block)
+            if (srem && bcnt == 0) {
+                refill();
+                const uint32_t k = srem < 4 ? srem : 4u;
+                bval = (uint32_t)bb;
+                bdst = pos;
+                bcnt = k;
+                drop(8 * k);
+                pos += k;
+                srem -= k;
+            }
+            if (srem == 0 && bcnt == 0) {
+                if (sfull) {
+                    result = full_status;
+                    st = S_DONE;
+                } else if (sstarve) {
+                    st = S_DONE;
+                } else {
+                    st = S_TYPE;
+                }
+            }
+        }
+        // ================================================== D. dynamic header
+        if (st == S_DYN) {
+            // TABLE / LENLENS (inflate_stream.ipp:222-262)
+            refill();
+            int32_t avail = tb + (int32_t)nb;
+            if (avail < 14) {
+                st = S_DONE;
+            } else {
+                nlen = ((uint32_t)bb & 31u) + 257;
+                ndist = ((uint32_t)(bb >> 5) & 31u) + 1;
+                const uint32_t ncode = ((uint32_t)(bb >> 10) & 15u) + 4;
+                drop(14);
+                avail -= 14;
+                if (nlen > 286 || ndist > 30) {
+                    result = ST_TOO_MANY_SYMBOLS;
+                    st = S_DONE;
+                } else if (avail < (int32_t)(3 * ncode)) {
+                    st = S_DONE;
+                } else {
+                    // the 19 code-length-code lengths, 3 bits each by symbol
+                    uint64_t clp = 0;
+                    refill();
+#pragma unroll
+                    for (int i = 0; i < 10; ++i)
+                        clp |= (uint64_t)((uint32_t)i < ncode ? ((uint32_t)(bb >> (3 * i)) & 7u) : 0u)
+                               << (3 * kClenOrder2[i]);
+                    drop(3 * (ncode < 10 ? ncode : 10u));
+                    refill();
+#pragma unroll
+                    for (int i = 10; i < 19; ++i)
+                        clp |= (uint64_t)((uint32_t)i < ncode ? ((uint32_t)(bb >> (3 * (i - 10))) & 7u) : 0u)
+                               << (3 * kClenOrder2[i]);
+                    drop(3 * (ncode > 10 ? ncode - 10 : 0u));
+                    // code-length code (inflate_stream.ipp:249-262)
+                    uint64_t acc = 0;
+#pragma unroll
+                    for (int i = 0; i < 19; ++i) acc += 1ull << (5 * ((clp >> (3 * i)) & 7u));
+                    uint32_t c[16];
+#pragma unroll
+                    for (int l = 0; l < 16; ++l) c[l] = (l >= 1 && l <= 7) ? (uint32_t)(acc >> (5 * l)) & 31u : 0u;
+                    const int e = make_canon<7>(c, 7, 0, tc);
+                    cl_empty = c[1] + c[2] + c[3] + c[4] + c[5] + c[6] + c[7] == 0;
+                    if (e) {
+                        result = e;
+                        st = S_DONE;
+                    } else {
+                        uint64_t offs = 0;   // first canonical index per length, 5 bits each
+                        uint32_t cu = 0;
+#pragma unroll
+                        for (int l = 1; l <= 7; ++l) {
+                            offs |= (uint64_t)cu << (5 * l);
+                            cu += c[l];
+                        }
+#pragma unroll
+                        for (int i = 0; i < 19; ++i) {
+                            const uint32_t l = (uint32_t)(clp >> (3 * i)) & 7u;
+                            const uint32_t at = (uint32_t)(offs >> (5 * l)) & 31u;
+                            offs += 1ull << (5 * l);
+                            if (l) T[O_CLS + at] = (uint8_t)i;
+                        }
+                        uint64_t* nib = (uint64_t*)(T + O_NIB);
+#pragma unroll
+                        for (int k = 0; k < 20; ++k) nib[k] = 0;
+                        uint4* h4 = (uint4*)H;
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) h4[k] = make_uint4(0, 0, 0, 0);
+                        want = nlen + ndist;
+                        have = 0;
+                        prev = 0;
+                        eob_seen = false;
+                        st = S_PASS1;
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int kc = 0; kc < KCL; ++kc) {
+            if (st != S_PASS1 || st0 != S_PASS1) break;
+                // CODELENS (inflate_stream.ipp:264-327), up to KCL symbols per iteration
+                refill();
+                const int32_t avail = tb + (int32_t)nb;
+                uint32_t L = 1, csym = 0;
+                if (!cl_empty) {
+                    const uint32_t c7 = __builtin_bitreverse32((uint32_t)bb) >> 25;
+                    const Sym yc = canon_decode<7>(tc.Q, c7);
+                    L = yc.L;
+                    csym = T[O_CLS + (yc.idx < 19 ? yc.idx : 0u)];
+                }
+                if (avail < (int32_t)tc.root) {
+                    st = S_DONE;
+                } else {
+                    uint32_t val = csym, rep = 1, used = L;
+                    bool ok = true;
+                    if (csym >= 16) {
+                        const uint32_t xb = csym == 16 ? 2u : (csym == 17 ? 3u : 7u);
+                        if (avail < (int32_t)(L + xb)) {
+                            st = S_DONE;
+                            ok = false;
+                        } else {
+                            const uint32_t x = (uint32_t)(bb >> L) & lowmask(xb);
+                            used = L + xb;
+                            if (csym == 16) {
+                                if (have == 0) {
+                                    result = ST_INVALID_BIT_LENGTH_REPEAT;
+                                    st = S_DONE;
+                                    ok = false;
+                                }
+                                val = prev;
+                                rep = 3 + x;
+                            } else {
+                                val = 0;
+                                rep = (csym == 17 ? 3u : 11u) + x;
+                            }
+                            if (ok && have + rep > want) {
+                                result = ST_INVALID_BIT_LENGTH_REPEAT;
+                                st = S_DONE;
+                                ok = false;
+                            }
+                        }
+                    }
+                    if (ok) {
+                        drop(used);
+                        if (val) {
+                            const uint32_t a = have, b = have + rep;
+                            const uint64_t pat = ((uint64_t)val * 0x1111111111111111ull) & ((1ull << (4 * rep)) - 1);
+                            const uint64_t v = pat << ((a & 7) * 4);
+                            uint32_t* nw = (uint32_t*)(T + O_NIB) + (a >> 3);
+                            __hip_atomic_fetch_or(nw, (uint32_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            if ((uint32_t)(v >> 32))
+                                __hip_atomic_fetch_or(nw + 1, (uint32_t)(v >> 32), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+                            const uint32_t e_l = b < nlen ? b : nlen;
+                            const uint32_t nl = e_l > a ? e_l - a : 0u;
+                            const uint32_t e_o = b < 256 ? b : 256u;
+                            const uint32_t nlo = e_o > a ? e_o - a : 0u;
+                            const uint32_t s_d = a > nlen ? a : nlen;
+                            const uint32_t nd = b > s_d ? b - s_d : 0u;
+                            __hip_atomic_fetch_add(H + val, nl | (nlo << 10) | (nd << 20), __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+                            if (a <= 256 && 256 < b) eob_seen = true;
+                        }
+                        prev = val;
+                        have += rep;
+                        if (have == want) st = S_BUILD;
+                    }
+                }
+        }
+        if (st == S_BUILD) {
+            if (!eob_seen) {
+                result = ST_MISSING_EOB;
+                st = S_DONE;
+            } else {
+                uint32_t h[16];
+                const uint4* h4 = (const uint4*)H;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint4 v = h4[k];
+                    h[4 * k] = v.x;
+                    h[4 * k + 1] = v.y;
+                    h[4 * k + 2] = v.z;
+                    h[4 * k + 3] = v.w;
+                }
+                uint32_t c[16];
+                c[0] = 0;
+#pragma unroll
+                for (int l = 1; l < 16; ++l) c[l] = h[l] & 0x3ffu;
+                int e = make_canon<15>(c, 9, 1, tl);
+                if (!e) {
+#pragma unroll
+                    for (int l = 1; l < 16; ++l) c[l] = (h[l] >> 20) & 0x3ffu;
+                    e = make_canon<15>(c, 6, 2, td);
+                }
+                if (e) {
+                    result = e;
+                    st = S_DONE;
+                } else {
+                    // litend (first canonical index past the literals of each length)
+                    // and the placement cursors (first index of each length)
+                    uint32_t cl_ = 0, cd_ = 0;
+#pragma unroll
+                    for (int l = 0; l < 16; l += 2) {
+                        const uint32_t a0 = l ? h[l] : 0u, a1 = h[l + 1];
+                        const uint32_t le0 = cl_ + ((a0 >> 10) & 0x3ffu);
+                        H[l] = cl_ | (cd_ << 16);
+                        cl_ += a0 & 0x3ffu;
+                        cd_ += (a0 >> 20) & 0x3ffu;
+                        const uint32_t le1 = cl_ + ((a1 >> 10) & 0x3ffu);
+                        H[l + 1] = cl_ | (cd_ << 16);
+                        cl_ += a1 & 0x3ffu;
+                        cd_ += (a1 >> 20) & 0x3ffu;
+                        ((uint32_t*)LE)[l >> 1] = le0 | (le1 << 16);
+                    }
+                    have = 0;
+                    st = S_PASS2;
+                }
+            }
+        }
+        if (st == S_PASS2) {
+            // place symbols in canonical order (inflate_stream.ipp:632-640)
+#pragma unroll
+            for (uint32_t h8 = 0; h8 < KNIB; h8 += 8) {
+                const uint32_t w = ((const uint32_t*)(T + O_NIB))[(have + h8) >> 3];
+                uint32_t olds[8];
+                // all fetch-adds first (no branch between them), then the
+                // placements: one LDS round trip for the eight
+#pragma unroll
+                for (uint32_t k = 0; k < 8; ++k) {
+                    const uint32_t i = have + h8 + k;
+                    const uint32_t l = (w >> (4 * k)) & 15u;
+                    const uint32_t inc = (l && i < want) ? (i < nlen ? 1u : 0x10000u) : 0u;
+                    olds[k] = __hip_atomic_fetch_add(H + l, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+#pragma unroll
+                for (uint32_t k = 0; k < 8; ++k) {
+                    const uint32_t i = have + h8 + k;
+                    const uint32_t l = (w >> (4 * k)) & 15u;
+                    if (l && i < want) {
+                        if (i < nlen) T[O_LIT + (olds[k] & 0xffffu)] = (uint8_t)i;
+                        else T[O_DST + (olds[k] >> 16)] = (uint8_t)(i - nlen);
+                    }
+                }
+            }
+            have += KNIB;
+            if (have >= want) st = S_DATA;
+        }
+
+    }
+}
+
+}  // namespace lp2
+}  // namespace bpmd
+
+// max_in != 0: only payloads of at most max_in bytes (the rest go to the wave
+// kernel, pmd_capi.hip).  order: NULL or the message order (e.g. longest
+// first); qctr: NULL (one message per lane, slot = message) or a zeroed
+// device counter for the work queue.
+extern "C" int bpmd_internal_inflate_lane2(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n,
+                                           uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                                           uint32_t* out_len, int32_t* status, uint32_t raw, const uint32_t* mask_key,
+                                           const uint32_t* hist_len, uint32_t hist_max, uint32_t max_in,
+                                           const uint32_t* order, uint32_t* qctr, uint32_t grid_waves,
+                                           hipStream_t stream)
+{
+    using namespace bpmd::lp2;
+    if (n == 0) return 0;
+    unsigned grid = (n + LPW - 1) / LPW;
+    if (qctr && grid_waves && grid > grid_waves) grid = grid_waves;
+    hipLaunchKernelGGL(inflate_lane2_kernel, dim3(grid), dim3(64), LPW * STRIDE, stream, in, in_off, in_len, n, out,
+                       out_off, out_cap, out_len, status, raw, mask_key, hist_len, hist_max, max_in, order, qctr);
+    return (int)hipGetLastError();
+}

@@ -365,7 +365,7 @@ def main():
     value = uncomp * world / (1 << 30) / step_s
     alg_bytes = comp + uncomp + 16 * n
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    kname = "inflate_lane_kernel" if n >= 2048 else "inflate_kernel"   # bpmd_set_inflate_kernel(0) policy
+    kname = "inflate_lane3_kernel" if n >= 2048 else "inflate_kernel"   # bpmd_set_inflate_kernel(0) policy
     traffic, traffic_src = pmc_traffic(kname) if n == N_MSGS else (None, None)
     # (traffic_src: the PMC file, its raw FETCH/WRITE bytes and the FETCH calibration used)
     result = {
