@@ -6,6 +6,7 @@
 
 #include <atomic>
 #include <mutex>
+#include <vector>
 
 #include "../../include/beast_pmd.h"
 
@@ -30,6 +31,7 @@ extern "C" int bpmd_internal_inflate_lane3(const uint8_t* in, const uint64_t* in
                                            uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                                            uint32_t* out_len, int32_t* status, uint32_t raw, const uint32_t* mask_key,
                                            const uint32_t* hist_len, uint32_t hist_max, uint32_t max_in,
+                                           const uint32_t* order, uint32_t* qctr, uint32_t grid_wgs,
                                            hipStream_t stream);
 extern "C" int bpmd_internal_inflate_lane2(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n,
                                            uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
@@ -64,6 +66,42 @@ extern "C" int bpmd_internal_slide(uint8_t* buf, const uint64_t* base, const uin
 namespace {
 std::mutex g_init_mu;
 int g_init_device = -1;   // device whose symbols are initialised
+
+// Per (device, stream) scratch for batch calls that need device workspace
+// (the inflate work queue's counter and message order).  Allocated on first
+// use and grown when a larger batch arrives; calls on one stream are ordered
+// by the stream, calls on different streams use different scratch.
+struct Scratch {
+    int dev;
+    hipStream_t stream;
+    uint8_t* p;
+    size_t cap;
+};
+std::mutex g_scratch_mu;
+std::vector<Scratch> g_scratch;
+
+uint8_t* scratch_for(hipStream_t s, size_t bytes)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    for (auto& e : g_scratch)
+        if (e.dev == dev && e.stream == s) {
+            if (e.cap >= bytes) return e.p;
+            // the stream may still use the old block: free it once the stream is idle
+            if (hipStreamSynchronize(s) != hipSuccess) return nullptr;
+            (void)hipFree(e.p);
+            e.p = nullptr;
+            e.cap = 0;
+            if (hipMalloc(&e.p, bytes) != hipSuccess) return nullptr;
+            e.cap = bytes;
+            return e.p;
+        }
+    uint8_t* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    g_scratch.push_back(Scratch{dev, s, p, bytes});
+    return p;
+}
 }
 
 extern "C" const char* bpmd_version(void) { return "beast_pmd 0.2 (gfx950)"; }
@@ -166,9 +204,28 @@ int inflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
     // split, and no second launch (C2 +1.6 %, C4 lane-only 23.2 vs 22.6 GiB/s)
     const uint32_t split = (hist || m != 0 || n_msgs >= 32768) ? 0u : inflate_split();
     int e = 0;
-    if (lane && lane_design() == 3)
+    if (lane && lane_design() == 3) {
+        // more messages than the chip holds lanes: a work queue keeps every
+        // lane busy until the batch is done (mixed sizes, configs[3])
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        uint32_t wgs = 4u * (uint32_t)cus;   // 4 workgroups of 64 messages per CU are resident
+        // diagnostics / tests: BPMD_QUEUE_WGS caps the grid so that small batches
+        // run through the work queue too
+        static const uint32_t q_override = [] {
+            const char* e = getenv("BPMD_QUEUE_WGS");
+            return e ? (uint32_t)strtoul(e, nullptr, 10) : 0u;
+        }();
+        if (q_override) wgs = q_override;
+        uint32_t* qctr = nullptr;
+        if (n_msgs > wgs * 64u && !split) {
+            qctr = (uint32_t*)scratch_for(s, 256);
+            if (!qctr || hipMemsetAsync(qctr, 0, sizeof(uint32_t), s) != hipSuccess) return BPMD_R_HIP_ERROR;
+        }
         e = bpmd_internal_inflate_lane3(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
-                                        d_status, raw, key, hist, 1u << cfg->window_bits, split, s);
+                                        d_status, raw, key, hist, 1u << cfg->window_bits, split, nullptr, qctr, wgs,
+                                        s);
+    }
     else if (lane && lane_design() == 2)
         e = bpmd_internal_inflate_lane2(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
                                         d_status, raw, key, hist, 1u << cfg->window_bits, split, nullptr, nullptr, 0u,

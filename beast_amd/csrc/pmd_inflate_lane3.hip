@@ -56,7 +56,10 @@ constexpr unsigned O_HEAD = 624;   // u32      tokens written (decoder)
 constexpr unsigned O_TAIL = 628;   // u32      tokens taken (expander)
 constexpr unsigned STRIDE = 632;   // x 64 lanes x 4 workgroups = 161 792 B per CU
 constexpr unsigned RING = 32;
-constexpr uint32_t TOK_END = 0x80000000u;
+constexpr unsigned WG_MSGS = 64;
+constexpr uint32_t TOK_END = 0x80000000u;   // word 0: out_len, bits 0-7: status
+constexpr uint32_t TOK_NEW = 0x40000000u;   // word 0: the message the lane starts (work queue)
+constexpr uint32_t TOK_EXIT = 0x20000000u;  // the queue is empty: the lane is done
 
 #ifndef BPMD3_KLIT
 #define BPMD3_KLIT 4
@@ -292,16 +295,18 @@ static __constant__ const uint8_t kClenOrder2[19] = {16, 17, 18, 0, 8, 7, 9, 6, 
 __device__ __forceinline__ void expander(uint8_t* T, bool valid, uint32_t m, uint8_t* __restrict__ out,
                                          const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
                                          uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
-                                         const uint32_t* __restrict__ hist_len, uint32_t hist_max)
+                                         const uint32_t* __restrict__ hist_len, uint32_t hist_max, bool queue)
 {
     uint8_t* o = out;
     uint32_t cap = 0, hist = 0;
-    if (valid) {
-        o = out + out_off[m];
-        cap = out_cap[m];
-        hist = hist_len ? (hist_len[m] < hist_max ? hist_len[m] : hist_max) : 0u;
-    }
-    bool done = !valid;
+    auto slot = [&](uint32_t mm) {
+        o = out + out_off[mm];
+        cap = out_cap[mm];
+        hist = hist_len ? (hist_len[mm] < hist_max ? hist_len[mm] : hist_max) : 0u;
+    };
+    if (valid) slot(m);
+    bool done = !valid;            // the lane's message is complete (END taken)
+    bool exited = !queue && done;  // no token will come any more
     uint32_t tail = 0, pos = 0;
     // match copy: bytes left to issue, distance, next output position
     uint32_t crem = 0, cdist = 0, cq = 0;
@@ -315,7 +320,7 @@ __device__ __forceinline__ void expander(uint8_t* T, bool valid, uint32_t m, uin
     uint32_t bcnt = 0, bdst = 0, bval = 0;
     L3_DECL;
     for (;;) {
-        const bool alive = !done || crem != 0 || cst || bcnt != 0;
+        const bool alive = !exited || crem != 0 || cst || bcnt != 0;
         if (!__ballot(alive)) break;
         L3_CNT(1);
         bool worked = cst || bcnt != 0 || crem != 0;
@@ -406,12 +411,17 @@ __device__ __forceinline__ void expander(uint8_t* T, bool valid, uint32_t m, uin
             }
         }
         // ================================================ next token
-        if (!done && crem == 0) {
+        if (!exited && crem == 0) {
             const uint32_t head = lds_load(T + O_HEAD);
             compiler_fence();
+            uint2 e = make_uint2(0, 0);
             if (tail != head) {
-                const uint2 e = *(const uint2*)(T + ring_at(tail));
+                e = *(const uint2*)(T + ring_at(tail));
                 compiler_fence();
+            }
+            // a NEW token switches the output slot: the previous message's
+            // pending stores go out first
+            if (tail != head && !((e.y & TOK_NEW) && (cst || bcnt != 0))) {
                 ++tail;
                 lds_store(T + O_TAIL, tail);
                 worked = true;
@@ -419,6 +429,14 @@ __device__ __forceinline__ void expander(uint8_t* T, bool valid, uint32_t m, uin
                     out_len[m] = e.x;
                     status[m] = (int32_t)(int8_t)(e.y & 0xffu);
                     done = true;
+                    exited = !queue;
+                } else if (e.y & TOK_NEW) {
+                    m = e.x;
+                    slot(m);
+                    pos = 0;
+                    done = false;
+                } else if (e.y & TOK_EXIT) {
+                    exited = true;
                 } else {
                     const uint32_t nl = e.y & 7u, ml = (e.y >> 3) & 511u;
                     if (nl) {
@@ -450,47 +468,27 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
                                         const uint64_t* __restrict__ in_off, const uint32_t* __restrict__ in_len,
                                         const uint32_t* __restrict__ out_cap, uint32_t raw,
                                         const uint32_t* __restrict__ mask_key, const uint32_t* __restrict__ hist_len,
-                                        uint32_t hist_max)
+                                        uint32_t hist_max, uint32_t n_msgs, const uint32_t* __restrict__ order,
+                                        uint32_t* __restrict__ qctr)
 {
     uint32_t* H = (uint32_t*)(T + O_HIST);
     uint16_t* LE = (uint16_t*)(T + O_LE);
     const uint32_t tail = raw ? 0u : 4u;
     const int32_t full_status = raw ? ST_OK : ST_NEED_BUFFERS;
-    const uint8_t* p = in;
-    uint32_t n = 0, cap = 0;
-    if (valid) {
-        p = in + in_off[m];
-        n = in_len[m];
-        cap = out_cap[m];
-    }
-    const uint32_t s = (uint32_t)((uintptr_t)p & 3);
-    const uint8_t* A = p - s;
-    // masked payloads (bpmd_read_batch): the dword at A + 4k holds payload
-    // bytes 4k - s .. 4k - s + 3, masked with key bytes (j - s) % 4
-    // (mask.ipp:38-59), so one rotation of the key unmasks every dword
-    const uint32_t mk =
-        (valid && mask_key) ? __builtin_amdgcn_alignbit(mask_key[m], mask_key[m], 8u * ((0u - s) & 3u)) : 0u;
-    // context takeover (bpmd_inflate_takeover_batch): the hist bytes before the
-    // slot are the window Beast's inflater keeps across messages
-    const uint32_t hist = (valid && hist_len) ? (hist_len[m] < hist_max ? hist_len[m] : hist_max) : 0u;
+    // per-message state (set by begin())
+    const uint8_t* A = in;
+    uint32_t s = 0, n = 0, cap = 0, mk = 0, hist = 0;
     // bit reader: bb holds up to 64 bits; refills take 32-bit words from q
     // (a 16-byte block, shifted down as it is used), then from nx (the next
     // block, already in registers).  Blocks move nx <- sg <- memory only in
     // the loop's memory section, so decoding never waits on memory.
     uint4 q = make_uint4(0, 0, 0, 0), nx = q, sg = q;
-    if (valid) {
-        const uint4 b0w = issue_block(A, 0, s, n), b1w = issue_block(A, 1, s, n);
-        q = finish_block(make_uint4(b0w.x ^ mk, b0w.y ^ mk, b0w.z ^ mk, b0w.w ^ mk), 0, s, n, tail);
-        nx = finish_block(make_uint4(b1w.x ^ mk, b1w.y ^ mk, b1w.z ^ mk, b1w.w ^ mk), 1, s, n, tail);
-    }
-    const uint32_t E_in = (s + n + 3) & ~3u;
-    bool sg_ld = valid && 32 < E_in;
-    if (sg_ld) sg = *(const uint4*)(A + 32 - 4 * in_shift(32, E_in));
+    bool sg_ld = false;
     uint32_t blk = 3, qn = 4, sg_bi = 2;
     bool nx_used = false;
     uint64_t bb = 0;
     uint32_t nb = 0;
-    int32_t tb = (int32_t)(8 * (s + n + tail));   // stream bits not yet moved into bb
+    int32_t tb = 0;   // stream bits not yet moved into bb
     auto refill = [&]() {   // branchless: in a wave some lane nearly always needs it
         const bool need = nb <= 32;
         const uint64_t add = (uint64_t)q.x << (nb & 63);
@@ -534,34 +532,95 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
         bb >>= k;
         nb -= k;
     };
-    refill();
-    refill();
-    drop(8 * s);
-
-    uint32_t st = valid ? (raw && n == 0 ? S_DONE : S_TYPE) : S_DONE;
-    int32_t result = (valid && raw && n == 0) ? ST_NEED_BUFFERS : ST_OK;
-    bool last = false, fin = !valid;   // fin: END token written
+    uint32_t st = S_DONE;
+    int32_t result = ST_OK;
+    bool last = false, fin = true;   // fin: END token written
     uint32_t pos = 0, head = 0;
     Canon<15> tl, td;
     Canon<7> tc;
-#pragma unroll
-    for (int i = 0; i < 15; ++i) { tl.Q[i] = 0; td.Q[i] = 0; }
-    tl.root = 9;
-    td.root = 5;
-#pragma unroll
-    for (int i = 0; i < 7; ++i) tc.Q[i] = 0;
-    tc.root = 1;
     // header state
     uint32_t nlen = 0, ndist = 0, want = 0, have = 0, prev = 0;
     bool eob_seen = false, cl_empty = false;
     // stored block
     uint32_t srem = 0;
     bool sfull = false, sstarve = false;
+    // work queue (qctr != null): a lane whose END token is out takes the next
+    // message; its NEW token tells the expander which slot to write; a lane
+    // that finds the queue empty sends EXIT
+    uint32_t msg = m;
+    bool send_new = false, send_exit = false, exhausted = qctr == nullptr;
+    const uint32_t first_slots = gridDim.x * WG_MSGS;
+    auto begin = [&](uint32_t mm) {
+        msg = mm;
+        const uint8_t* p = in + in_off[mm];
+        n = in_len[mm];
+        cap = out_cap[mm];
+        s = (uint32_t)((uintptr_t)p & 3);
+        A = p - s;
+        // masked payloads (bpmd_read_batch): the dword at A + 4k holds payload
+        // bytes 4k - s .. 4k - s + 3, masked with key bytes (j - s) % 4
+        // (mask.ipp:38-59), so one rotation of the key unmasks every dword
+        mk = mask_key ? __builtin_amdgcn_alignbit(mask_key[mm], mask_key[mm], 8u * ((0u - s) & 3u)) : 0u;
+        // context takeover (bpmd_inflate_takeover_batch): the hist bytes before
+        // the slot are the window Beast's inflater keeps across messages
+        hist = hist_len ? (hist_len[mm] < hist_max ? hist_len[mm] : hist_max) : 0u;
+        const uint4 b0w = issue_block(A, 0, s, n), b1w = issue_block(A, 1, s, n);
+        q = finish_block(make_uint4(b0w.x ^ mk, b0w.y ^ mk, b0w.z ^ mk, b0w.w ^ mk), 0, s, n, tail);
+        nx = finish_block(make_uint4(b1w.x ^ mk, b1w.y ^ mk, b1w.z ^ mk, b1w.w ^ mk), 1, s, n, tail);
+        const uint32_t E_in = (s + n + 3) & ~3u;
+        sg_ld = 32 < E_in;
+        if (sg_ld) sg = *(const uint4*)(A + 32 - 4 * in_shift(32, E_in));
+        blk = 3;
+        qn = 4;
+        sg_bi = 2;
+        nx_used = false;
+        bb = 0;
+        nb = 0;
+        tb = (int32_t)(8 * (s + n + tail));
+        refill();
+        refill();
+        drop(8 * s);
+        st = raw && n == 0 ? S_DONE : S_TYPE;
+        result = raw && n == 0 ? ST_NEED_BUFFERS : ST_OK;
+        last = false;
+        fin = false;
+        pos = 0;
+#pragma unroll
+        for (int i = 0; i < 15; ++i) { tl.Q[i] = 0; td.Q[i] = 0; }
+        tl.root = 9;
+        td.root = 5;
+#pragma unroll
+        for (int i = 0; i < 7; ++i) tc.Q[i] = 0;
+        tc.root = 1;
+        srem = 0;
+    };
+    if (valid) begin(m);
 
-    L3_DECL;
-    L3_LAPDECL;
     for (;;) {
-        if (!__ballot(!fin)) break;
+        if (!exhausted) {
+            const uint64_t idle = __ballot(fin && !send_new && !exhausted);
+            // take new messages when a quarter of the wave waits or nothing else runs
+            if (idle && (__builtin_popcountll(idle) * 4 >= 64 || __ballot(!fin) == 0)) {
+                const unsigned leader = (unsigned)__builtin_ctzll(idle);
+                uint32_t base = 0;
+                if ((threadIdx.x & 63u) == leader) base = atomicAdd(qctr, (uint32_t)__builtin_popcountll(idle));
+                base = __shfl(base, (int)leader);
+                if ((idle >> (threadIdx.x & 63u)) & 1) {
+                    const uint32_t k =
+                        first_slots + base + (uint32_t)__builtin_popcountll(idle & ((1ull << (threadIdx.x & 63u)) - 1ull));
+                    if (k < n_msgs) {
+                        // the NEW token goes out first; the message begins once it is
+                        // in the ring (its header may need the ring's LDS)
+                        msg = order ? order[k] : k;
+                        send_new = true;
+                    } else {
+                        exhausted = true;
+                        send_exit = true;
+                    }
+                }
+            }
+        }
+        if (!__ballot(!fin || send_new || send_exit)) break;
         L3_LAP(3);
         L3_CNT(1);
 #ifdef BPMD_PROF
@@ -1087,7 +1146,16 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
 
         L3_LAP(2);
         // ---- publish the token (entry first, then head)
-        if (enl || emlen) {
+        if (send_new || send_exit) {
+            if (head - taken < RING) {
+                *(uint2*)(T + ring_at(head)) = make_uint2(msg, send_new ? TOK_NEW : TOK_EXIT);
+                compiler_fence();
+                lds_store(T + O_HEAD, ++head);
+                if (send_new) begin(msg);
+                send_new = false;
+                send_exit = false;
+            }
+        } else if (enl || emlen) {
             *(uint2*)(T + ring_at(head)) = make_uint2(elit, enl | (emlen << 3) | (edist << 12));
             compiler_fence();
             lds_store(T + O_HEAD, ++head);
@@ -1108,53 +1176,57 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
 }
 
 // A workgroup is one decoder wave and one expander wave over 64 messages;
-// four workgroups per CU.  (One workgroup of 4 decoders + 4 expanders per CU,
-// which pins a decoder and an expander to every SIMD, measured slower: 117
-// vs 130 GiB/s on C2.)
-constexpr unsigned WG_MSGS = 64;
-
+// four workgroups per CU (WG_MSGS).  (One workgroup of 4 decoders + 4
+// expanders per CU, which pins a decoder and an expander to every SIMD,
+// measured slower: 117 vs 130 GiB/s on C2.)
 __global__ void __launch_bounds__(128, 2)
 inflate_lane3_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                      const uint32_t* __restrict__ in_len, uint32_t n_msgs, uint8_t* __restrict__ out,
                      const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
                      uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t raw,
                      const uint32_t* __restrict__ mask_key, const uint32_t* __restrict__ hist_len, uint32_t hist_max,
-                     uint32_t max_in)
+                     uint32_t max_in, const uint32_t* __restrict__ order, uint32_t* __restrict__ qctr)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const unsigned lane = threadIdx.x & 63u;
     const bool is_decoder = threadIdx.x < 64;
-    const unsigned slot = lane;   // the message's slot in the workgroup
-    uint8_t* T = smem + slot * STRIDE;
-    const uint32_t m = blockIdx.x * WG_MSGS + slot;
+    uint8_t* T = smem + lane * STRIDE;
+    // first message: slot blockIdx.x * 64 + lane (of `order` when given)
+    const uint32_t j = blockIdx.x * WG_MSGS + lane;
+    bool valid = j < n_msgs;
+    const uint32_t m = valid ? (order ? order[j] : j) : 0u;
     // max_in != 0: only payloads of at most max_in bytes (the rest go to the
     // wave kernel, see inflate_impl in pmd_capi.hip)
-    bool valid = m < n_msgs;
     if (valid && max_in && in_len[m] > max_in) valid = false;
     if (is_decoder) *(uint2*)(T + O_HEAD) = make_uint2(0, 0);
     __syncthreads();
     if (is_decoder) {
         if (BPMD3_DPRIO) __builtin_amdgcn_s_setprio(BPMD3_DPRIO);   // the decoder sets the pace
-        decoder(T, valid, m, in, in_off, in_len, out_cap, raw, mask_key, hist_len, hist_max);
+        decoder(T, valid, m, in, in_off, in_len, out_cap, raw, mask_key, hist_len, hist_max, n_msgs, order, qctr);
+    } else {
+        expander(T, valid, m, out, out_off, out_cap, out_len, status, hist_len, hist_max, qctr != nullptr);
     }
-    else
-        expander(T, valid, m, out, out_off, out_cap, out_len, status, hist_len, hist_max);
 }
 
 }  // namespace lp3
 }  // namespace bpmd
 
+// order: NULL or the order messages are taken in (e.g. longest first);
+// qctr: NULL (one message per lane) or a zeroed device counter: then the grid
+// is at most grid_wgs workgroups and lanes take further messages from it.
 extern "C" int bpmd_internal_inflate_lane3(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n,
                                            uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                                            uint32_t* out_len, int32_t* status, uint32_t raw, const uint32_t* mask_key,
                                            const uint32_t* hist_len, uint32_t hist_max, uint32_t max_in,
+                                           const uint32_t* order, uint32_t* qctr, uint32_t grid_wgs,
                                            hipStream_t stream)
 {
     using namespace bpmd::lp3;
     if (n == 0) return 0;
-    const unsigned grid = (n + WG_MSGS - 1) / WG_MSGS;
+    unsigned grid = (n + WG_MSGS - 1) / WG_MSGS;
+    if (qctr && grid_wgs && grid > grid_wgs) grid = grid_wgs;
     hipLaunchKernelGGL(inflate_lane3_kernel, dim3(grid), dim3(128), WG_MSGS * STRIDE, stream, in, in_off, in_len, n,
-                       out, out_off, out_cap, out_len, status, raw, mask_key, hist_len, hist_max, max_in);
+                       out, out_off, out_cap, out_len, status, raw, mask_key, hist_len, hist_max, max_in, order, qctr);
     return (int)hipGetLastError();
 }
 

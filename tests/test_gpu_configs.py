@@ -106,3 +106,32 @@ def test_deflate_roundtrip_and_size(cfg):
     _, _, clen, _ = O.deflate_batch(data, off, lens, level=level, wbits=15, mem_level=4, threads=16)
     ours, beast = int(plen.sum()), int(clen.astype(np.uint64).sum())
     assert ours <= SIZE_TOLERANCE * beast, (ours, beast, ours / beast)
+
+
+def test_c4_work_queue_batch():
+    """More messages than the chip's resident lanes (65 536): the lane kernel's
+    work queue hands the rest out as lanes finish.  Oracle payloads of a
+    C4-shaped batch (sizes capped at 8 KiB to keep the oracle quick), inflated
+    on the GPU: every message equals the oracle's inflate."""
+    import torch
+    from beast_amd import pmd
+    n = 70000
+    lens = np.minimum(synth.zipf_sizes(n, 0x5EED0044), 8192).astype(np.uint32)
+    raw, off, ln = synth.make_batch("json", lens, seed=0x5EED0044)
+    comp, coff, clen, st = O.deflate_batch(raw, off, ln, level=6, mem_level=4, threads=16)
+    assert (st == 0).all()
+    for kernel in (0, 1):
+        assert pmd.lib().bpmd_set_inflate_kernel(kernel) == 0
+        try:
+            src = pmd.Batch.from_arrays(comp, coff.astype(np.int64), clen.astype(np.int32))
+            cap = torch.from_numpy(ln.astype(np.int32)).cuda()
+            r = pmd.inflate_batch(src, cap)
+            torch.cuda.synchronize()
+            assert int((r.status != 0).sum()) == 0
+            assert torch.equal(r.out.len.cpu(), torch.from_numpy(ln.astype(np.int32)))
+            outs = r.out.data.cpu().numpy()
+            o_off = r.out.off.cpu().numpy()
+            got = np.concatenate([outs[int(o_off[i]):int(o_off[i]) + int(ln[i])] for i in range(n)])
+            assert np.array_equal(got, raw[:int(ln.astype(np.int64).sum())])
+        finally:
+            pmd.lib().bpmd_set_inflate_kernel(0)
