@@ -74,19 +74,20 @@ int g_init_device = -1;   // device whose symbols are initialised
 struct Scratch {
     int dev;
     hipStream_t stream;
+    int which;
     uint8_t* p;
     size_t cap;
 };
 std::mutex g_scratch_mu;
 std::vector<Scratch> g_scratch;
 
-uint8_t* scratch_for(hipStream_t s, size_t bytes)
+uint8_t* scratch_for(hipStream_t s, size_t bytes, int which = 0)
 {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
     std::lock_guard<std::mutex> lk(g_scratch_mu);
     for (auto& e : g_scratch)
-        if (e.dev == dev && e.stream == s) {
+        if (e.dev == dev && e.stream == s && e.which == which) {
             if (e.cap >= bytes) return e.p;
             // the stream may still use the old block: free it once the stream is idle
             if (hipStreamSynchronize(s) != hipSuccess) return nullptr;
@@ -99,9 +100,16 @@ uint8_t* scratch_for(hipStream_t s, size_t bytes)
         }
     uint8_t* p = nullptr;
     if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
-    g_scratch.push_back(Scratch{dev, s, p, bytes});
+    g_scratch.push_back(Scratch{dev, s, which, p, bytes});
     return p;
 }
+}
+
+// scratch block `which` (0 inflate queue, 1-2 deflate workspace) for other
+// translation units
+extern "C" void* bpmd_internal_scratch(hipStream_t s, size_t bytes, int which)
+{
+    return scratch_for(s, bytes, which);
 }
 
 extern "C" const char* bpmd_version(void) { return "beast_pmd 0.2 (gfx950)"; }

@@ -36,6 +36,8 @@
 
 #include <mutex>
 
+#include <hipcub/hipcub.hpp>
+
 #include "pmd_common.h"
 #include "wave_util.h"
 #include "lz_core.h"
@@ -561,6 +563,7 @@ struct MsgOut {
     unsigned cbits;    // valid bits in carry
     bool overflow;
     uint32_t key;      // masking key, 0 = unmasked: payload byte j ^= key >> 8 (j % 4) (mask.ipp:38-59)
+    bool stored;       // the last chunk was written as a stored block
 };
 
 __device__ __forceinline__ void put_bytes_global(MsgOut& o, const uint8_t* src_lds, unsigned ob, unsigned nbytes)
@@ -937,11 +940,13 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
         o.opos += total;
         o.carry = 0;
         o.cbits = 0;
+        o.stored = true;
         pf.lap(11);
         return;
     }
 
     // ---- Huffman block: codes table = fixed or dynamic
+    o.stored = false;
     if (kind == 1) {
         for (unsigned i = lane; i < N_LCODES; i += WAVE) {
             unsigned l;
@@ -1104,6 +1109,168 @@ deflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
     pf.flush();
 }
 
+// ------------------------------------------------ chunk-parallel large messages
+// A message longer than one chunk (or any message of a context-takeover
+// batch) is encoded chunk by chunk IN PARALLEL: every 4 KiB chunk, with the
+// 4 KiB of input before it as history, becomes one block of its own in a
+// scratch slot, starting at bit 0 (deflate_chunks_kernel); then one wave per
+// message stitches the blocks together at their bit offsets, applies the
+// client mask and appends Flush::sync's empty stored block header
+// (stitch_kernel).  A block's contents and its stored/fixed/dynamic choice do
+// not depend on where it starts, so the payload is bit for bit the one the
+// serial chunk walk produced; only a stored block's padding to a byte
+// boundary depends on its start, and the stitch writes it there.
+constexpr unsigned SLOT = 4736;   // >= bpmd_deflate_upper_bound(CHUNK) + 2, 16-byte multiple
+#ifndef BPMD_CHUNK_HIST
+#define BPMD_CHUNK_HIST 4096
+#endif
+constexpr int CHUNK_HIST = BPMD_CHUNK_HIST;   // history bytes before each chunk (and before a takeover message)
+
+__device__ __forceinline__ uint32_t chunk_count(uint32_t len, bool all)
+{
+    return (all || len > CHUNK) ? (len + CHUNK - 1) / CHUNK : 0u;
+}
+
+struct ChunkCountOp {
+    const uint32_t* len;
+    uint32_t n;
+    bool all;
+    __host__ __device__ uint32_t operator()(uint32_t i) const
+    {
+        return i < n ? ((all || len[i] > CHUNK) ? (len[i] + CHUNK - 1) / CHUNK : 0u) : 0u;
+    }
+};
+
+__global__ void __launch_bounds__(256) count_chunks_kernel(const uint32_t* __restrict__ in_len, uint32_t n, uint32_t all,
+                                                           uint32_t* __restrict__ total)
+{
+    uint32_t c = 0;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        c += chunk_count(in_len[i], all != 0);
+    c = wave_sum(c);
+    if (lane_id() == 0 && c) atomicAdd(total, c);
+}
+
+__global__ void __launch_bounds__(256) fill_items_kernel(const uint32_t* __restrict__ in_len, uint32_t n, uint32_t all,
+                                                         const uint32_t* __restrict__ first, uint32_t* __restrict__ items)
+{
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t k = chunk_count(in_len[i], all != 0), f = first[i];
+        for (uint32_t c = 0; c < k; ++c) items[f + c] = i;
+    }
+}
+
+template <int HIST>
+__global__ void __launch_bounds__(64)
+deflate_chunks_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                      const uint32_t* __restrict__ in_len, const uint32_t* __restrict__ items,
+                      const uint32_t* __restrict__ first, const uint32_t* __restrict__ n_items,
+                      uint8_t* __restrict__ temp, uint32_t* __restrict__ bits, uint32_t* __restrict__ qctr, Params P)
+{
+    __shared__ DefLds<HIST> S;
+    Prof pf;
+    const uint32_t total = *n_items;
+    // chunks from a counter: 5 waves per CU leave one SIMD with two, whose
+    // waves would set the end of a static stride
+    auto next = [&]() -> uint32_t {
+        uint32_t v = 0;
+        if (lane_id() == 0) v = atomicAdd(qctr, 1u);
+        return (uint32_t)__shfl((int)v, 0);
+    };
+    for (uint32_t k = next(); k < total; k = next()) {
+        const uint32_t i = items[k];
+        const uint32_t c = k - first[i];
+        const uint32_t len = in_len[i];
+        const unsigned hist = P.hist_len ? (P.hist_len[i] < (unsigned)HIST ? P.hist_len[i] : (unsigned)HIST) : 0u;
+        MsgOut o;
+        o.dst = temp + (size_t)k * SLOT;
+        o.cap = SLOT;
+        o.opos = 0;
+        o.carry = 0;
+        o.cbits = 0;
+        o.overflow = false;
+        o.key = 0;
+        o.stored = false;
+        deflate_chunk<HIST>(S, in + in_off[i], c * CHUNK, len, hist, P, o, pf);
+        if (lane_id() == 0)
+            bits[k] = o.overflow ? 0xFFFFFFFFu : ((o.stored ? 0x80000000u : 0u) | (o.opos * 8 + o.cbits));
+        wave_sync();
+    }
+    pf.flush();
+}
+
+// one wave per large message: its chunk blocks at their bit offsets
+__global__ void __launch_bounds__(64)
+stitch_kernel(const uint32_t* __restrict__ in_len, uint32_t n, uint32_t all, const uint32_t* __restrict__ first,
+              const uint8_t* __restrict__ temp, const uint32_t* __restrict__ bits, uint8_t* __restrict__ out,
+              const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
+              uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t* __restrict__ out_bits,
+              const uint32_t* __restrict__ mask_key)
+{
+    const unsigned lane = lane_id();
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const uint32_t len = in_len[i];
+        if (!all && len <= CHUNK) continue;
+        const uint32_t nk = chunk_count(len, all != 0), f = first[i];
+        uint8_t* o = out + out_off[i];
+        const uint32_t cap = out_cap[i];
+        const uint32_t key = mask_key ? mask_key[i] : 0u;
+        auto km = [&](uint32_t p) { return (uint8_t)(key >> (8 * (p & 3))); };
+        uint32_t bit = 0;   // output bits so far
+        uint32_t cv = 0;    // the partial byte at bit >> 3 (its low bit & 7 bits)
+        bool overflow = false;
+        for (uint32_t c = 0; c < nk && !overflow; ++c) {
+            const uint32_t k = f + c;
+            const uint32_t w = bits[k];
+            if (w == 0xFFFFFFFFu) { overflow = true; break; }
+            const uint8_t* t = temp + (size_t)k * SLOT;
+            const uint32_t L = w & 0x7FFFFFFFu;
+            const uint32_t B = bit >> 3, s = bit & 7;
+            if (w & 0x80000000u) {
+                // stored block: 000 at `bit`, pad to a byte, then LEN NLEN and the
+                // bytes (in the slot from byte 1: header + pad took byte 0)
+                const uint32_t P = (bit + 3 + 7) >> 3;
+                const uint32_t nbytes = L / 8 - 1;
+                if (P + nbytes + 1 > cap) { overflow = true; break; }
+                if (lane == 0) {
+                    o[B] = (uint8_t)cv ^ km(B);
+                    if (P - B == 2) o[B + 1] = km(B + 1);
+                }
+                for (uint32_t j = lane; j < nbytes; j += WAVE) o[P + j] = t[1 + j] ^ km(P + j);
+                bit = (P + nbytes) * 8;
+                cv = 0;
+            } else {
+                const uint32_t end = bit + L;
+                if (((end + 7) >> 3) + 1 > cap) { overflow = true; break; }
+                const uint32_t nb = (L + 7) >> 3;             // slot bytes
+                const uint32_t full = (end >> 3) - B;         // output bytes completed by this block
+                auto tb = [&](uint32_t j) -> uint32_t { return j < nb ? t[j] : 0u; };
+                auto val = [&](uint32_t j) -> uint32_t {
+                    const uint32_t lo = s == 0 ? 0u : (j == 0 ? cv : tb(j - 1) >> (8 - s));
+                    return ((tb(j) << s) | lo) & 0xFFu;
+                };
+                for (uint32_t j = lane; j < full; j += WAVE) o[B + j] = (uint8_t)val(j) ^ km(B + j);
+                cv = (end & 7) ? val(full) : 0u;
+                bit = end;
+            }
+        }
+        // Flush::sync's empty stored block header (000) + pad; 00 00 FF FF stripped
+        const uint32_t tbytes = (bit & 7) + 3 > 8 ? 2u : 1u;
+        const uint32_t olen = (bit >> 3) + tbytes;
+        if (!overflow && olen > cap) overflow = true;
+        if (lane == 0) {
+            if (!overflow) {
+                o[bit >> 3] = (uint8_t)cv ^ km(bit >> 3);
+                if (tbytes == 2) o[(bit >> 3) + 1] = km((bit >> 3) + 1);
+            }
+            out_len[i] = overflow ? 0u : olen;
+            if (out_bits) out_bits[i] = overflow ? 0u : bit;
+            status[i] = overflow ? ST_NEED_BUFFERS : ST_OK;
+        }
+        wave_sync();
+    }
+}
+
 }  // namespace dfl
 }  // namespace bpmd
 
@@ -1112,6 +1279,7 @@ deflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
 #endif
 
 extern "C" unsigned bpmd_diag_grid_override;
+extern "C" void* bpmd_internal_scratch(hipStream_t s, size_t bytes, int which);
 // diagnostic: 1 = history kernel on a static grid stride (no work queue)
 extern "C" unsigned bpmd_deflate_static_grid;
 unsigned bpmd_deflate_static_grid = 0;   // pmd_capi.hip; 0 = size the grid by occupancy
@@ -1190,11 +1358,85 @@ int deflate_impl(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_l
     P.out_bits = out_bits;
     P.mask_key = mask_key;
     P.hist_len = hist_len;
+    static const bool serial = [] {
+        const char* e = getenv("BPMD_DEFLATE_SERIAL");   // A/B: the round-1 serial chunk walk
+        return e && e[0] == '1';
+    }();
+    if (serial) {
+        P.chain = chain(true);
+        int e = launch<0>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, P, stream);
+        if (e) return e;
+        P.chain = chain(false);
+        return launch<4096>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, P, stream);
+    }
+    using namespace bpmd::dfl;
+    const uint32_t all = hist_len ? 1u : 0u;   // context takeover: every message needs its history window
+    // how many chunk blocks the large messages make (one small read back: it
+    // sizes the workspace; the single-chunk kernel is enqueued right after it
+    // and runs meanwhile)
+    uint32_t* d_total = (uint32_t*)bpmd_internal_scratch(stream, 256, 1);   // [0] chunk count, [32] chunk queue
+    if (!d_total) return (int)hipErrorOutOfMemory;
+    hipError_t he = hipMemsetAsync(d_total, 0, 256, stream);
+    if (he != hipSuccess) return (int)he;
+    hipLaunchKernelGGL(count_chunks_kernel, dim3(n < 256 * 256 ? (n + 255) / 256 : 256), dim3(256), 0, stream, in_len, n,
+                       all, d_total);
+    // a pinned word per host thread, so the copy is asynchronous and the event covers it
+    thread_local uint32_t* h_total = nullptr;
+    if (!h_total && hipHostMalloc((void**)&h_total, 64, hipHostMallocDefault) != hipSuccess) return (int)hipErrorOutOfMemory;
+    hipEvent_t ev = nullptr;
+    if ((he = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return (int)he;
+    if ((he = hipMemcpyAsync(h_total, d_total, sizeof(uint32_t), hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+        (he = hipEventRecord(ev, stream)) != hipSuccess) {
+        (void)hipEventDestroy(ev);
+        return (int)he;
+    }
     P.chain = chain(true);
-    int e = launch<0>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, P, stream);
+    int e = all ? 0 : launch<0>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, P, stream);
+    he = hipEventSynchronize(ev);
+    (void)hipEventDestroy(ev);
     if (e) return e;
+    if (he != hipSuccess) return (int)he;
+    const uint32_t total = *h_total;
+    const bool big = total > 0 || all;
+    if (!big) {
+        // the stitch also finishes zero-chunk messages only on the takeover path
+        return 0;
+    }
+    // workspace: first[n + 1] | items[total] | bits[total] | slots[total] | scan temp
+    size_t cub_bytes = 0;
+    hipcub::CountingInputIterator<uint32_t> idx(0);
+    hipcub::TransformInputIterator<uint32_t, ChunkCountOp, hipcub::CountingInputIterator<uint32_t>> counts(
+        idx, ChunkCountOp{in_len, n, all != 0});
+    if ((he = hipcub::DeviceScan::ExclusiveSum(nullptr, cub_bytes, counts, (uint32_t*)nullptr, n + 1, stream)) !=
+        hipSuccess)
+        return (int)he;
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o_first = 0, o_items = up(o_first + 4ull * (n + 1)), o_bits = up(o_items + 4ull * total),
+                 o_slots = up(o_bits + 4ull * total), o_cub = up(o_slots + (size_t)SLOT * total),
+                 bytes = up(o_cub + cub_bytes);
+    uint8_t* ws = (uint8_t*)bpmd_internal_scratch(stream, bytes, 2);
+    if (!ws) return (int)hipErrorOutOfMemory;
+    uint32_t* first = (uint32_t*)(ws + o_first);
+    uint32_t* items = (uint32_t*)(ws + o_items);
+    uint32_t* bits = (uint32_t*)(ws + o_bits);
+    uint8_t* slots = ws + o_slots;
+    if ((he = hipcub::DeviceScan::ExclusiveSum(ws + o_cub, cub_bytes, counts, first, n + 1, stream)) != hipSuccess)
+        return (int)he;
+    const unsigned fgrid = n < 256 * 1024 ? (n + 255) / 256 : 1024;
+    hipLaunchKernelGGL(fill_items_kernel, dim3(fgrid), dim3(256), 0, stream, in_len, n, all, first, items);
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     P.chain = chain(false);
-    return launch<4096>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, P, stream);
+    if (total) {
+        const unsigned per_cu = (160u * 1024u) / (unsigned)sizeof(DefLds<CHUNK_HIST>);
+        const unsigned grid = total < (uint32_t)cus * per_cu ? total : (unsigned)cus * per_cu;
+        hipLaunchKernelGGL(deflate_chunks_kernel<CHUNK_HIST>, dim3(grid), dim3(64), 0, stream, in, in_off, in_len, items,
+                           first, d_total, slots, bits, d_total + 32, P);
+    }
+    const unsigned sgrid = n < (uint32_t)cus * 16 ? n : (unsigned)cus * 16;
+    hipLaunchKernelGGL(stitch_kernel, dim3(sgrid), dim3(64), 0, stream, in_len, n, all, first, slots, bits, out, out_off,
+                       out_cap, out_len, status, out_bits, mask_key);
+    return (int)hipGetLastError();
 }
 }  // namespace
 
