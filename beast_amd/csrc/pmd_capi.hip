@@ -21,30 +21,12 @@ extern "C" int bpmd_internal_inflate_keyed_split(const uint8_t* in, const uint64
                                                  const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
                                                  uint32_t raw, const uint32_t* mask_key, uint32_t min_in,
                                                  hipStream_t stream);
-extern "C" int bpmd_internal_inflate_lane_split(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
-                                                uint32_t n, uint8_t* out, const uint64_t* out_off,
-                                                const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
-                                                uint32_t raw, const uint32_t* mask_key, const uint32_t* hist_len,
-                                                uint32_t hist_max, uint32_t max_in, hipStream_t stream);
-extern "C" int bpmd_internal_init_fixed_lane(void);
 extern "C" int bpmd_internal_inflate_lane3(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n,
                                            uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                                            uint32_t* out_len, int32_t* status, uint32_t raw, const uint32_t* mask_key,
                                            const uint32_t* hist_len, uint32_t hist_max, uint32_t max_in,
                                            const uint32_t* order, uint32_t* qctr, uint32_t grid_wgs,
                                            hipStream_t stream);
-extern "C" int bpmd_internal_inflate_lane2(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n,
-                                           uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
-                                           uint32_t* out_len, int32_t* status, uint32_t raw, const uint32_t* mask_key,
-                                           const uint32_t* hist_len, uint32_t hist_max, uint32_t max_in,
-                                           const uint32_t* order, uint32_t* qctr, uint32_t grid_waves,
-                                           hipStream_t stream);
-extern "C" int bpmd_internal_inflate_lane(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
-                                          uint32_t n, uint8_t* out, const uint64_t* out_off,
-                                          const uint32_t* out_cap, uint32_t* out_len, int32_t* status, uint32_t raw,
-                                          const uint32_t* mask_key, const uint32_t* hist_len, uint32_t hist_max,
-                                          hipStream_t stream);
-
 extern "C" int bpmd_internal_deflate_keyed(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                            uint32_t n, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                                            uint32_t* out_len, int32_t* status, int level, int window_bits,
@@ -119,7 +101,7 @@ extern "C" const char* bpmd_version(void) { return "beast_pmd 0.2 (gfx950)"; }
 extern "C" unsigned bpmd_diag_grid_override = 0;
 extern "C" void bpmd_diag_set_grid(unsigned grid) { bpmd_diag_grid_override = grid; }
 
-// Kernel choice for a batch: one lane per message (pmd_inflate_lane.hip)
+// Kernel choice for a batch: one lane per message (pmd_inflate_lane3.hip)
 // for throughput, one wave per message (pmd_inflate.hip) for latency when
 // the batch is too small to fill the chip's lanes.  BPMD_INFLATE=lane|wave
 // or bpmd_set_inflate_kernel() forces one (the tests run both).
@@ -148,17 +130,6 @@ static int inflate_mode()
 // idle, so payloads longer than the split (compressed bytes; several 4 KiB
 // chunks of output) go to the wave kernel and only batches of >= 2048
 // messages use lanes at all; batches of >= 32 Ki messages use lanes only.  BPMD_INFLATE_SPLIT overrides the split.
-// Lane kernel design: 2 = pmd_inflate_lane2.hip (default), 1 = the round-1
-// kernel (pmd_inflate_lane.hip); BPMD_LANE overrides (A/B only).
-static int lane_design()
-{
-    static const int d = [] {
-        const char* e = getenv("BPMD_LANE");
-        return (e && !strcmp(e, "1")) ? 1 : (e && !strcmp(e, "2")) ? 2 : 3;
-    }();
-    return d;
-}
-
 static uint32_t inflate_split()
 {
     const char* e = getenv("BPMD_INFLATE_SPLIT");
@@ -174,7 +145,6 @@ extern "C" int bpmd_init(void)
     std::lock_guard<std::mutex> lk(g_init_mu);
     if (g_init_device == dev) return BPMD_R_OK;
     if (bpmd_internal_init_fixed() != 0) return BPMD_R_HIP_ERROR;
-    if (bpmd_internal_init_fixed_lane() != 0) return BPMD_R_HIP_ERROR;
     g_init_device = dev;
     return BPMD_R_OK;
 }
@@ -212,7 +182,7 @@ int inflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
     // split, and no second launch (C2 +1.6 %, C4 lane-only 23.2 vs 22.6 GiB/s)
     const uint32_t split = (hist || m != 0 || n_msgs >= 32768) ? 0u : inflate_split();
     int e = 0;
-    if (lane && lane_design() == 3) {
+    if (lane) {
         // more messages than the chip holds lanes: a work queue keeps every
         // lane busy until the batch is done (mixed sizes, configs[3])
         int dev = 0, cus = 256;
@@ -234,13 +204,6 @@ int inflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
                                         d_status, raw, key, hist, 1u << cfg->window_bits, split, nullptr, qctr, wgs,
                                         s);
     }
-    else if (lane && lane_design() == 2)
-        e = bpmd_internal_inflate_lane2(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
-                                        d_status, raw, key, hist, 1u << cfg->window_bits, split, nullptr, nullptr, 0u,
-                                        s);
-    else if (lane)
-        e = bpmd_internal_inflate_lane_split(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
-                                             d_status, raw, key, hist, 1u << cfg->window_bits, split, s);
     if (!e && (!lane || split))
         e = bpmd_internal_inflate_keyed_split(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap,
                                               d_out_len, d_status, raw, key, lane ? split : 0u, s);

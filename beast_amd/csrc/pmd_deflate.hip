@@ -107,17 +107,7 @@ struct Params {
     uint32_t* out_bits;  // optional: payload length in bits before the sync-marker tail
     const uint32_t* mask_key;   // optional: mask payload i with key i on the way out (write.hpp:679-685)
     const uint32_t* hist_len;   // optional (context takeover): plaintext bytes before message i usable as history
-    uint32_t* queue;     // optional: message counter of this launch (waves take the next message as they finish)
 };
-
-// Per-launch message counters for the history kernel's work queue: the host
-// zeroes slot k on the launch's stream and passes it in Params::queue, so
-// launches in flight on other streams use other slots.  A slot holds one
-// counter (own 128-byte line) per contiguous partition of the batch; wave w
-// takes messages from partition w % QUEUE_PARTS, so the single-chunk messages
-// it skips cost an atomic on one of 64 lines rather than all on one.
-constexpr unsigned QUEUE_SLOTS = 256, QUEUE_PARTS = 64, QUEUE_STRIDE = 32;
-__device__ uint32_t g_queue[QUEUE_SLOTS * QUEUE_PARTS * QUEUE_STRIDE];
 
 // Diagnostic build only (-DBPMD_PROF): per-phase wave cycles and counts.
 __device__ unsigned long long g_dprof[24];
@@ -1055,33 +1045,19 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
     pf.lap(15);
 }
 
-template <int HIST>
+// one wave per single-chunk message (<= CHUNK bytes, no takeover history)
 __global__ void __launch_bounds__(64)
 deflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint32_t* __restrict__ in_len,
                uint32_t n, uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
                const uint32_t* __restrict__ out_cap, uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
                Params P)
 {
-    __shared__ DefLds<HIST> S;
+    __shared__ DefLds<0> S;
     const unsigned lane = lane_id();
     Prof pf;
-    // multi-chunk messages vary from 2 to 16+ chunks: waves take them from a
-    // queue so no wave is left with a run of large ones (grid stride otherwise)
-    const unsigned part = blockIdx.x % QUEUE_PARTS;
-    const uint32_t plo = (uint32_t)((uint64_t)n * part / QUEUE_PARTS);
-    const uint32_t phi = (uint32_t)((uint64_t)n * (part + 1) / QUEUE_PARTS);
-    auto next = [&](uint32_t strided) -> uint32_t {
-        if (!P.queue) return strided;
-        uint32_t v = 0;
-        if (lane == 0) v = atomicAdd(P.queue + part * QUEUE_STRIDE, 1u);
-        v = (uint32_t)__shfl((int)v, 0);
-        return v < phi - plo ? plo + v : n;
-    };
-    for (uint32_t i = next(blockIdx.x); i < n; i = next(i + gridDim.x)) {
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
         const uint32_t len = in_len[i];
-        // context takeover needs the history window: all its messages take the HIST kernel
-        if (HIST == 0 ? (len > CHUNK || P.hist_len) : (len <= CHUNK && !P.hist_len)) continue;
-        const unsigned hist = P.hist_len ? (P.hist_len[i] < (unsigned)HIST ? P.hist_len[i] : (unsigned)HIST) : 0u;
+        if (len > CHUNK) continue;   // chunk-parallel path (deflate_chunks_kernel + stitch_kernel)
         MsgOut o;
         o.dst = out + out_off[i];
         o.cap = out_cap[i];
@@ -1091,7 +1067,7 @@ deflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
         o.overflow = false;
         o.key = P.mask_key ? P.mask_key[i] : 0u;
         const uint8_t* msg = in + in_off[i];
-        for (uint32_t base = 0; base < len && !o.overflow; base += CHUNK) deflate_chunk<HIST>(S, msg, base, len, hist, P, o, pf);
+        if (len) deflate_chunk<0>(S, msg, 0, len, 0u, P, o, pf);
         // Flush::sync's empty stored block header (000) + pad; 00 00 FF FF stripped
         const unsigned tb = o.cbits + 3 > 8 ? 2u : 1u;
         if (!o.overflow && o.opos + tb > o.cap) o.overflow = true;
@@ -1118,13 +1094,10 @@ deflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
 // client mask and appends Flush::sync's empty stored block header
 // (stitch_kernel).  A block's contents and its stored/fixed/dynamic choice do
 // not depend on where it starts, so the payload is bit for bit the one the
-// serial chunk walk produced; only a stored block's padding to a byte
+// serial walk over the chunks would produce; only a stored block's padding to a byte
 // boundary depends on its start, and the stitch writes it there.
 constexpr unsigned SLOT = 4736;   // >= bpmd_deflate_upper_bound(CHUNK) + 2, 16-byte multiple
-#ifndef BPMD_CHUNK_HIST
-#define BPMD_CHUNK_HIST 4096
-#endif
-constexpr int CHUNK_HIST = BPMD_CHUNK_HIST;   // history bytes before each chunk (and before a takeover message)
+constexpr int CHUNK_HIST = 4096;   // history bytes before each chunk (and before a takeover message)
 
 __device__ __forceinline__ uint32_t chunk_count(uint32_t len, bool all)
 {
@@ -1274,58 +1247,23 @@ stitch_kernel(const uint32_t* __restrict__ in_len, uint32_t n, uint32_t all, con
 }  // namespace dfl
 }  // namespace bpmd
 
-#ifndef BPMD_HIST_WPC
-#define BPMD_HIST_WPC 4
-#endif
-
 extern "C" unsigned bpmd_diag_grid_override;
 extern "C" void* bpmd_internal_scratch(hipStream_t s, size_t bytes, int which);
-// diagnostic: 1 = history kernel on a static grid stride (no work queue)
-extern "C" unsigned bpmd_deflate_static_grid;
-unsigned bpmd_deflate_static_grid = 0;   // pmd_capi.hip; 0 = size the grid by occupancy
 
 namespace {
-template <int HIST>
-int launch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n, uint8_t* out,
-           const uint64_t* out_off, const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
-           const bpmd::dfl::Params& P, hipStream_t stream)
+// single-chunk messages: as many waves as the LDS holds, grid-strided
+int launch_single(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n, uint8_t* out,
+                  const uint64_t* out_off, const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
+                  const bpmd::dfl::Params& P, hipStream_t stream)
 {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const unsigned per_cu = (160u * 1024u) / (unsigned)sizeof(bpmd::dfl::DefLds<HIST>);
-    // the history kernel fits 5 waves per CU by LDS, but 5 waves on 4 SIMDs
-    // leave one SIMD shared and its waves set the end of the launch (C5:
-    // 7.0 GiB/s at 5, 10.7 at 4)
-    const unsigned cap_cu = HIST ? (unsigned)BPMD_HIST_WPC : per_cu;
-    unsigned grid = (unsigned)cus * (per_cu ? (per_cu < cap_cu ? per_cu : cap_cu) : 1u);
+    const unsigned per_cu = (160u * 1024u) / (unsigned)sizeof(bpmd::dfl::DefLds<0>);
+    unsigned grid = (unsigned)cus * (per_cu ? per_cu : 1u);
     if (bpmd_diag_grid_override) grid = bpmd_diag_grid_override;
     if (grid > n) grid = n;
-    bpmd::dfl::Params Q = P;
-    Q.queue = nullptr;
-    if (HIST && n > grid && grid >= bpmd::dfl::QUEUE_PARTS && !bpmd_deflate_static_grid) {
-        // g_queue is a __device__ variable: one copy, at its own address, per
-        // device.  Its QUEUE_SLOTS counter slots are handed out round-robin,
-        // so at most QUEUE_SLOTS history launches may be in flight at once
-        // (over all streams) on one device.
-        static std::atomic<unsigned> seq{0};
-        static std::mutex mu;
-        static uint32_t* bases[64] = {};
-        uint32_t* base = nullptr;
-        if (dev >= 0 && dev < 64) {
-            std::lock_guard<std::mutex> lk(mu);
-            if (!bases[dev] && hipGetSymbolAddress((void**)&bases[dev], HIP_SYMBOL(bpmd::dfl::g_queue)) != hipSuccess)
-                bases[dev] = nullptr;
-            base = bases[dev];
-        }
-        if (base) {
-            constexpr unsigned words = bpmd::dfl::QUEUE_PARTS * bpmd::dfl::QUEUE_STRIDE;
-            Q.queue = base + (seq.fetch_add(1u) % bpmd::dfl::QUEUE_SLOTS) * words;
-            if (hipMemsetAsync(Q.queue, 0, words * sizeof(uint32_t), stream) != hipSuccess)
-                return (int)hipGetLastError();
-        }
-    }
-    hipLaunchKernelGGL(bpmd::dfl::deflate_kernel<HIST>, dim3(grid), dim3(64), 0, stream, in, in_off, in_len, n, out,
-                       out_off, out_cap, out_len, status, Q);
+    hipLaunchKernelGGL(bpmd::dfl::deflate_kernel, dim3(grid), dim3(64), 0, stream, in, in_off, in_len, n, out, out_off,
+                       out_cap, out_len, status, P);
     return (int)hipGetLastError();
 }
 }  // namespace
@@ -1358,17 +1296,6 @@ int deflate_impl(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_l
     P.out_bits = out_bits;
     P.mask_key = mask_key;
     P.hist_len = hist_len;
-    static const bool serial = [] {
-        const char* e = getenv("BPMD_DEFLATE_SERIAL");   // A/B: the round-1 serial chunk walk
-        return e && e[0] == '1';
-    }();
-    if (serial) {
-        P.chain = chain(true);
-        int e = launch<0>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, P, stream);
-        if (e) return e;
-        P.chain = chain(false);
-        return launch<4096>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, P, stream);
-    }
     using namespace bpmd::dfl;
     const uint32_t all = hist_len ? 1u : 0u;   // context takeover: every message needs its history window
     // how many chunk blocks the large messages make (one small read back: it
@@ -1391,7 +1318,7 @@ int deflate_impl(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_l
         return (int)he;
     }
     P.chain = chain(true);
-    int e = all ? 0 : launch<0>(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, P, stream);
+    int e = all ? 0 : launch_single(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, P, stream);
     he = hipEventSynchronize(ev);
     (void)hipEventDestroy(ev);
     if (e) return e;
