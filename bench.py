@@ -109,7 +109,8 @@ def cpu_baselines(comp_buf, comp_off, comp_len, raw_lens, raw3, off3, len3, targ
     and C3 messages (deflate, L6/mem4/w15 + pmd framing): the C restatement
     of Beast's zlib ("port", byte-identical to Beast at L1-9) and the
     reference's own zlib 1.3.1 ("reference", compiled from
-    test/extern/zlib-1.3.1 by oracle/Makefile), each at 1 thread and at T
+    test/extern/zlib-1.3.1 by oracle/Makefile) and, as an extra column, the
+    image's system zlib behind the same shim ("system"), each at 1 thread and at T
     threads = the cores this process may use (capped at 16, the box's share
     for one GPU).  Per measurement the sample is sized for ~target_s of CPU
     work; median of 3, outputs preallocated (oracle.time_batch)."""
@@ -135,7 +136,7 @@ def cpu_baselines(comp_buf, comp_off, comp_len, raw_lens, raw3, off3, len3, targ
 
     for name, inflate in (("inflate", True), ("deflate", False)):
         r = {}
-        for impl in ("port", "reference"):
+        for impl in ("port", "reference", "system"):
             one = leg(impl, inflate, 1)
             many = leg(impl, inflate, T) if one else None
             if one:
@@ -145,6 +146,8 @@ def cpu_baselines(comp_buf, comp_off, comp_len, raw_lens, raw3, off3, len3, targ
                     r["_beast_len"] = many["out_len"]
                 if inflate:   # the sample decodes exactly (every message is 4096 bytes)
                     r[impl]["exact"] = bool((one["out_len"] == MSG_BYTES).all())
+        if "system" in r:
+            r["system"]["version"] = O.zsys().zref_version().decode()
         if "port" in r and "reference" in r:
             # calibration: per-byte time of the port relative to zlib 1.3.1 on one core
             r["t_port_over_t_zlib_1thread"] = round(r["reference"]["1_thread"] / r["port"]["1_thread"], 3)
@@ -502,7 +505,8 @@ def main():
                 result["deflate"]["cpu_baseline"] = {
                     "value": dcpu["port"][f"{T}_threads"], "unit": "GiB/s", "cores": T, "kind": "port",
                     "sample": f"C3 messages, {dcpu['port'][f'sample_{T}']}, L6/mem4/w15 + pmd framing",
-                    "one_thread": dcpu["port"]["1_thread"], "reference_zlib_1.3.1": dcpu.get("reference")}
+                    "one_thread": dcpu["port"]["1_thread"], "reference_zlib_1.3.1": dcpu.get("reference"),
+                    "system_zlib": dcpu.get("system")}
         del src3, out3, rt_out, d, rr
 
     # --------------------------------- C4 / C5 shapes (configs[3], configs[4])
@@ -520,6 +524,7 @@ def main():
                 "sample": f"C2 payloads, {icpu['port'][f'sample_{T}']} x {MSG_BYTES} B, oracle inflate "
                           f"(C restatement of Beast's zlib), {T} threads, median of 3",
                 "one_thread": icpu["port"]["1_thread"], "reference_zlib_1.3.1": icpu.get("reference"),
+                "system_zlib": icpu.get("system"),
                 "t_port_over_t_zlib_1thread": icpu.get("t_port_over_t_zlib_1thread"),
                 "cpu_model": cpu["cpu_model"], "nproc": cpu["nproc"], "cores_available": cpu["cores_available"]}
     if rank == 0:

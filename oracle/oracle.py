@@ -79,25 +79,42 @@ def lib():
     return _LIB
 
 
+def _load_zshim(path):
+    if not os.path.exists(path):
+        return None
+    R = ctypes.CDLL(path)
+    R.zref_deflate.argtypes = [ctypes.c_int] * 5 + [ctypes.c_void_p, ctypes.c_ulong,
+                                                   ctypes.c_void_p, ctypes.c_ulong]
+    R.zref_deflate.restype = ctypes.c_long
+    R.zref_inflate.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_ulong, ctypes.c_void_p,
+                               ctypes.c_ulong, ctypes.POINTER(ctypes.c_int)]
+    R.zref_inflate.restype = ctypes.c_long
+    vp = ctypes.c_void_p
+    R.zref_batch.argtypes = [ctypes.c_int] * 4 + [vp] * 3 + [ctypes.c_uint32] + [vp] * 4 + [ctypes.c_int]
+    R.zref_batch.restype = ctypes.c_int
+    if hasattr(R, "zref_version"):
+        R.zref_version.restype = ctypes.c_char_p
+    return R
+
+
 def ref():
     """The reference's own zlib 1.3.1 (None when it could not be built)."""
     global _REF
     if _REF is None:
-        path = os.path.join(HERE, "_ref", "libzref.so")
-        if not os.path.exists(path):
-            return None
-        R = ctypes.CDLL(path)
-        R.zref_deflate.argtypes = [ctypes.c_int] * 5 + [ctypes.c_void_p, ctypes.c_ulong,
-                                                       ctypes.c_void_p, ctypes.c_ulong]
-        R.zref_deflate.restype = ctypes.c_long
-        R.zref_inflate.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_ulong, ctypes.c_void_p,
-                                   ctypes.c_ulong, ctypes.POINTER(ctypes.c_int)]
-        R.zref_inflate.restype = ctypes.c_long
-        vp = ctypes.c_void_p
-        R.zref_batch.argtypes = [ctypes.c_int] * 4 + [vp] * 3 + [ctypes.c_uint32] + [vp] * 4 + [ctypes.c_int]
-        R.zref_batch.restype = ctypes.c_int
-        _REF = R
+        _REF = _load_zshim(os.path.join(HERE, "_ref", "libzref.so"))
     return _REF
+
+
+_ZSYS = None
+
+
+def zsys():
+    """The image's system zlib behind the same shim (None when absent): an
+    extra CPU-baseline column, not a parity reference."""
+    global _ZSYS
+    if _ZSYS is None:
+        _ZSYS = _load_zshim(os.path.join(HERE, "libzsys.so"))
+    return _ZSYS
 
 
 class ZParams(ctypes.Structure):
@@ -362,7 +379,8 @@ def time_batch(impl: str, inflate: bool, data, off, lens, out_cap, threads=1, re
                mem_level=4):
     """Median wall seconds of one batch call on the host cores, outputs
     preallocated outside the timed region.  impl: "port" (this C restatement
-    of Beast's zlib) or "reference" (the reference's zlib 1.3.1, oracle/_ref).
+    of Beast's zlib), "reference" (the reference's zlib 1.3.1, oracle/_ref) or
+    "system" (the image's zlib, oracle/libzsys.so).
     Returns (seconds, out_len) or None when the implementation is absent."""
     import time
     n = len(lens)
@@ -376,8 +394,8 @@ def time_batch(impl: str, inflate: bool, data, off, lens, out_cap, threads=1, re
     data = np.ascontiguousarray(data, dtype=np.uint8)
     off = np.ascontiguousarray(off, dtype=np.uint64)
     lens = np.ascontiguousarray(lens, dtype=np.uint32)
-    if impl == "reference":
-        R = ref()
+    if impl in ("reference", "system"):
+        R = ref() if impl == "reference" else zsys()
         if R is None:
             return None
         call = lambda: R.zref_batch(1 if inflate else 0, level, wbits, mem_level, _p(data), _p(off), _p(lens), n,  # noqa: E731

@@ -7,7 +7,9 @@
  * restatement in bzo_deflate.c can be checked byte-for-byte (Beast == zlib
  * 1.3.1 at levels 1-9).
  */
-#define Z_PREFIX 1
+#ifndef ZREF_SYSTEM
+#define Z_PREFIX 1   /* libzref.so: the vendored zlib, prefixed; libzsys.so: the image's -lz */
+#endif
 #include "zlib.h"
 
 #include <string.h>
@@ -166,3 +168,6 @@ int zref_batch(int inflate_, int level, int wbits, int mem_level, const unsigned
     free(tid);
     return 0;
 }
+
+/* the zlib this shim was built against (1.3.1 for libzref, the image's for libzsys) */
+const char* zref_version(void) { return zlibVersion(); }
