@@ -101,6 +101,17 @@ template <int NB>
 __device__ __forceinline__ uint32_t canon_min(const uint32_t (&Q)[NB], uint32_t c)
 {
     const uint32_t k1 = (c + 1) << 15;
+#ifdef BPMD3_MIN3ASM
+    // v_min3 chain written out: the compiler otherwise splits part of it
+    // into two-operand mins
+    uint32_t d[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) d[i] = Q[i] - k1;
+    uint32_t m = d[0];
+#pragma unroll
+    for (int i = 1; i + 1 < NB; i += 2) asm("v_min3_u32 %0, %1, %2, %3" : "=v"(m) : "v"(m), "v"(d[i]), "v"(d[i + 1]));
+    if (NB % 2 == 0) m = __builtin_elementwise_min(m, d[NB - 1]);
+#else
     uint32_t m = Q[0] - k1;
 #pragma unroll
     for (int i = 1; i + 1 < NB; i += 2) {
@@ -108,6 +119,7 @@ __device__ __forceinline__ uint32_t canon_min(const uint32_t (&Q)[NB], uint32_t 
         m = __builtin_elementwise_min(m, __builtin_elementwise_min(x, y));
     }
     if (NB % 2 == 0) m = __builtin_elementwise_min(m, Q[NB - 1] - k1);
+#endif
     return m;
 }
 
@@ -297,6 +309,29 @@ __device__ __forceinline__ void expander(uint8_t* T, bool valid, uint32_t m, uin
                                          uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
                                          const uint32_t* __restrict__ hist_len, uint32_t hist_max, bool queue)
 {
+#ifdef BPMD3_EXP_MIN
+    // timing experiment: take tokens without expanding them (decoder alone)
+    {
+        bool ex = !queue && !valid;
+        uint32_t tl = 0;
+        for (;;) {
+            if (!__ballot(!ex)) break;
+            const uint32_t hd = lds_load(T + O_HEAD);
+            compiler_fence();
+            while (!ex && tl != hd) {
+                const uint2 e = *(const uint2*)(T + ring_at(tl));
+                ++tl;
+                if (e.y & TOK_END) { out_len[m] = e.x; status[m] = (int32_t)(int8_t)(e.y & 0xffu); ex = !queue; }
+                else if (e.y & TOK_NEW) m = e.x;
+                else if (e.y & TOK_EXIT) ex = true;
+            }
+            compiler_fence();
+            lds_store(T + O_TAIL, tl);
+            __builtin_amdgcn_s_sleep(BPMD3_ESLEEP);
+        }
+        return;
+    }
+#endif
     uint8_t* o = out;
     uint32_t cap = 0, hist = 0;
     auto slot = [&](uint32_t mm) {
@@ -402,6 +437,10 @@ __device__ __forceinline__ void expander(uint8_t* T, bool valid, uint32_t m, uin
                 cq += adv;
                 crem -= adv;
             }
+#ifdef BPMD3_EXP_NOMEM
+            ld = false;
+            cst = false;
+#endif
             if (ld) {
                 // 16 (32) bytes from src: the bytes used all lie in [src, cq);
                 // the rest may run into the next slot (never stored)
@@ -595,6 +634,8 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
         srem = 0;
     };
     if (valid) begin(m);
+    L3_DECL;
+    L3_LAPDECL;
 
     for (;;) {
         if (!exhausted) {
@@ -628,7 +669,10 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
 #endif
         // ---- the input pipeline (the only global memory the decoder touches)
         if (nx_used) {
-            nx = finish_in(sg, sg_ld, sg_bi, s, n, tail, mk);
+            // only a block that holds the payload's end needs finish_in's
+            // shift and tail work: a wave-uniform test keeps it off the rest
+            if (__ballot(sg_bi * 16 + 16 > s + n)) nx = finish_in(sg, sg_ld, sg_bi, s, n, tail, mk);
+            else nx = make_uint4(sg.x ^ mk, sg.y ^ mk, sg.z ^ mk, sg.w ^ mk);
             const uint32_t b0 = blk * 16, E = (s + n + 3) & ~3u;
             sg_ld = b0 < E;
             if (sg_ld) sg = *(const uint4*)(A + b0 - 4 * in_shift(b0, E));
@@ -687,11 +731,9 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
             uint32_t lit_bits = 0;
 #pragma unroll
             for (int k = 1; k <= KLIT; ++k) lit_bits = nlit == (uint32_t)k ? kp[k] : lit_bits;
-            if (nlit) {
-                enl = nlit;
-                elit = lbytes;
-                pos += nlit;
-            }
+            enl = nlit;
+            elit = lbytes;
+            pos += nlit;
             // the main token: symbol nlit (none when all KLIT were literals)
             uint32_t c15 = kc[0], L = kL[0], sym = ks[0];
             bool kinv_m = kinv[0];
@@ -705,104 +747,80 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
             }
             const bool inval = kinv_m || sym >= 286;
             drop_x(lit_bits);
-            if (nlit < (uint32_t)KLIT) {
-                refill();   // nb >= 33 again: the main token's <= 48 bits are in the window
-                const uint64_t w2 = nb >= 64 ? bb : (bb | ((uint64_t)q.x << nb));
-                const int32_t avail = tb + (int32_t)nb;
-                Sym y;
-                y.L = L;
-                y.idx = 0;
-                y.inval = inval;
-                // the fill rule only bites within 48 bits of the end of the input:
-                // a wave-uniform branch keeps its two canonical searches off the
-                // common path
-                const bool near_end = __ballot(avail < 48) != 0;
-                uint32_t need_l = 0;
-                if (near_end && avail < 48) need_l = canon_need<15>(tl, y, c15);
-                // length and distance are decoded for every lane (a wave nearly
-                // always holds a match): no divergent branch around them
-                const bool is_len = !inval && sym > 256;
-                const uint32_t li = is_len ? sym - 257 : 0u;
-                const uint32_t xl = (li < 8 || li == 28) ? 0u : ((li - 4) >> 2);
-                uint32_t len = li < 8 ? li + 3 : (li == 28 ? 258u : (((4u + (li & 3)) << xl) + 3));
-                len += (uint32_t)(w2 >> L) & lowmask(xl);
-                const uint32_t used = L + (is_len ? xl : 0u);
-                const uint32_t d15 = rev15(w2 >> used);
-                const Sym yd = canon_decode<15>(td.Q, d15);
-                const uint32_t Ld = yd.L;
-                const uint32_t dsym = T[O_DST + yd.idx];
-                const bool invd = yd.inval || dsym >= 30;
-                const uint32_t xd = dsym < 4 ? 0u : (dsym >> 1) - 1;
-                uint32_t dist = dsym < 4 ? dsym + 1 : (((2u + (dsym & 1)) << xd) + 1);
-                dist += (uint32_t)(w2 >> (used + Ld)) & lowmask(xd);
-                uint32_t need_d = 0;
-                if (near_end && avail < 48 && is_len) need_d = canon_need<15>(td, yd, d15);
-                bool is_match = false;
-                uint32_t ev = 0;   // 0 token, 1 eob, 2 starved, 3 error
-                int32_t err = 0;
-                uint32_t take = used;
-                if ((int32_t)need_l > avail) {
-                    ev = 2;
-                } else if (inval) {
-                    ev = 3;
-                    err = ST_INVALID_LITERAL_LENGTH;
-                } else if (sym == 256) {
-                    ev = 1;
-                } else if (sym > 256) {
-                    if ((int32_t)used > avail || (int32_t)(used + need_d) > avail) {
-                        ev = 2;
-                    } else if (invd) {
-                        ev = 3;
-                        err = ST_INVALID_DISTANCE_CODE;
-                    } else if ((int32_t)(used + Ld + xd) > avail) {
-                        ev = 2;
-                    } else {
-                        take = used + Ld + xd;
-                        is_match = true;
-                    }
-                }
-                drop_x(ev >= 2 ? 0u : take);
-                if (ev == 0) {
-                    // output checks in the reference's order (inflate_stream.ipp:475-514)
-                    if (raw && pos >= cap) {
-                        result = full_status;
-                        st = S_DONE;
-                    } else if (is_match && dist > pos + hist) {
-                        result = ST_INVALID_DISTANCE;
-                        st = S_DONE;
-                    } else if (pos >= cap) {
-                        result = full_status;
-                        st = S_DONE;
-                    } else {
-                        uint32_t olen = is_match ? len : 1u;
-                        if (pos + olen > cap) {
-                            olen = cap - pos;
-                            result = full_status;
-                            st = S_DONE;
-                        }
-                        if (is_match) {
-                            emlen = olen;
-                            edist = dist;
-                        } else {
-                            enl = 1;
-                            elit = sym;
-                        }
-                        pos += olen;
-                    }
-                } else if (ev == 1) {
-                    st = S_TYPE;
-                } else if (ev == 2) {
-                    st = S_DONE;
-                } else {
-                    result = err;
-                    st = S_DONE;
-                }
-            }
+            // The main token, for the lanes that have one (nlit < KLIT), without
+            // divergent branches: every outcome is a select (a branch costs the
+            // wave its exec-mask instructions whether or not a lane takes it).
+            const bool mt = nlit < (uint32_t)KLIT;
+            refill();   // nb >= 33 again: the main token's <= 48 bits are in the window
+            const uint64_t w2 = nb >= 64 ? bb : (bb | ((uint64_t)q.x << nb));
+            const int32_t avail = tb + (int32_t)nb;
+            Sym y;
+            y.L = L;
+            y.idx = 0;
+            y.inval = inval;
+            // the fill rule only bites within 48 bits of the end of the input:
+            // a wave-uniform branch keeps its two canonical searches off the
+            // common path
+            const bool near_end = __ballot(mt && avail < 48) != 0;
+            uint32_t need_l = 0;
+            if (near_end && mt && avail < 48) need_l = canon_need<15>(tl, y, c15);
+            const bool is_len = !inval && sym > 256;
+            const uint32_t li = is_len ? sym - 257 : 0u;
+            const uint32_t xl = (li < 8 || li == 28) ? 0u : ((li - 4) >> 2);
+            uint32_t len = li < 8 ? li + 3 : (li == 28 ? 258u : (((4u + (li & 3)) << xl) + 3));
+            len += (uint32_t)(w2 >> L) & lowmask(xl);
+            const uint32_t used = L + (is_len ? xl : 0u);
+            const uint32_t d15 = rev15(w2 >> used);
+            const Sym yd = canon_decode<15>(td.Q, d15);
+            const uint32_t Ld = yd.L;
+            const uint32_t dsym = T[O_DST + yd.idx];
+            const bool invd = yd.inval || dsym >= 30;
+            const uint32_t xd = dsym < 4 ? 0u : (dsym >> 1) - 1;
+            uint32_t dist = dsym < 4 ? dsym + 1 : (((2u + (dsym & 1)) << xd) + 1);
+            dist += (uint32_t)(w2 >> (used + Ld)) & lowmask(xd);
+            uint32_t need_d = 0;
+            if (near_end && mt && avail < 48 && is_len) need_d = canon_need<15>(td, yd, d15);
+            // event, in the reference's order: 0 token, 1 eob, 2 starved, 3 error
+            const bool s_m1 = (int32_t)used > avail || (int32_t)(used + need_d) > avail;
+            const bool s_m2 = (int32_t)(used + Ld + xd) > avail;
+            const uint32_t ev = (int32_t)need_l > avail ? 2u
+                                : inval               ? 3u
+                                : sym == 256          ? 1u
+                                : !is_len             ? 0u
+                                : s_m1                ? 2u
+                                : invd                ? 3u
+                                : s_m2                ? 2u
+                                                      : 0u;
+            const int32_t err = inval ? ST_INVALID_LITERAL_LENGTH : ST_INVALID_DISTANCE_CODE;
+            const bool is_match = ev == 0 && is_len;
+            drop_x(mt && ev < 2 ? (is_match ? used + Ld + xd : used) : 0u);
+            // output checks in the reference's order (inflate_stream.ipp:475-514)
+            const bool tok = mt && ev == 0;
+            const bool c_raw = raw && pos >= cap;
+            const bool c_dist = is_match && dist > pos + hist;
+            const bool c_full = pos >= cap;
+            uint32_t olen = is_match ? len : 1u;
+            const bool c_trunc = pos + olen > cap;
+            olen = c_trunc ? cap - pos : olen;
+            const bool emit = tok && !c_raw && !c_dist && !c_full;
+            const bool stop_full = tok && (c_raw || (!c_dist && (c_full || c_trunc)));
+            const bool stop_dist = tok && !c_raw && c_dist;
+            result = stop_full ? full_status : stop_dist ? ST_INVALID_DISTANCE : (mt && ev == 3) ? err : result;
+            st = (stop_full || stop_dist || (mt && ev >= 2)) ? (uint32_t)S_DONE : (mt && ev == 1) ? (uint32_t)S_TYPE : st;
+            emlen = emit && is_match ? olen : 0u;
+            edist = emit && is_match ? dist : 0u;
+            enl = emit && !is_match ? 1u : enl;
+            elit = emit && !is_match ? sym : elit;
+            pos += emit ? olen : 0u;
         }
 
 
         L3_LAP(1);
         // ======================================= block headers, stored
+        // (one wave-uniform branch skips the whole section while every lane
+        // is in a block's data or finished: a wave issues every instruction
+        // of the section's per-state tests otherwise, exec-mask work included)
+        if (__ballot(st0 != S_DATA && st0 != S_DONE)) {
         if (st == S_TYPE && st0 == S_TYPE) {
             if (last) {
                 result = ST_END_OF_STREAM;
@@ -1144,26 +1162,28 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
             if (have >= want) st = S_DATA;
         }
 
+        }   // block headers, stored
         L3_LAP(2);
         // ---- publish the token (entry first, then head)
-        if (send_new || send_exit) {
-            if (head - taken < RING) {
-                *(uint2*)(T + ring_at(head)) = make_uint2(msg, send_new ? TOK_NEW : TOK_EXIT);
-                compiler_fence();
-                lds_store(T + O_HEAD, ++head);
+        // (selects rather than an if-chain: one predicated store, one head store)
+        {
+            const bool ctl = send_new || send_exit;       // NEW / EXIT (work queue)
+            const bool data = !ctl && (enl || emlen);     // produced only with room
+            const bool endt = !ctl && !data && st == S_DONE && !fin;
+            const bool adv = room && (ctl || data || endt);
+            const uint2 ent = ctl    ? make_uint2(msg, send_new ? TOK_NEW : TOK_EXIT)
+                              : data ? make_uint2(elit, enl | (emlen << 3) | (edist << 12))
+                                     : make_uint2(pos, TOK_END | ((uint32_t)result & 0xffu));
+            if (adv) *(uint2*)(T + ring_at(head)) = ent;
+            compiler_fence();
+            head += adv ? 1u : 0u;
+            lds_store(T + O_HEAD, head);
+            fin = fin || (adv && endt);
+            if (adv && ctl) {
                 if (send_new) begin(msg);
                 send_new = false;
                 send_exit = false;
             }
-        } else if (enl || emlen) {
-            *(uint2*)(T + ring_at(head)) = make_uint2(elit, enl | (emlen << 3) | (edist << 12));
-            compiler_fence();
-            lds_store(T + O_HEAD, ++head);
-        } else if (st == S_DONE && !fin && room) {
-            *(uint2*)(T + ring_at(head)) = make_uint2(pos, TOK_END | ((uint32_t)result & 0xffu));
-            compiler_fence();
-            lds_store(T + O_HEAD, ++head);
-            fin = true;
         }
         // blocked on a full ring in every lane: leave the SIMD to the expander
         if (!__ballot(head != head0 || st != st0 || (st != S_DATA && st != S_SCOPY && st != S_DONE))) {

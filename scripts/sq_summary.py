@@ -1,4 +1,4 @@
-"""Per-design averages of the SQ counters collected by scripts/pmc_lane.sh
+"""Per-design averages of the SQ counters collected by scripts/pmc_lane3.sh
 for the lane inflate kernel (one C2 launch = 64 Ki messages)."""
 import collections
 import csv
