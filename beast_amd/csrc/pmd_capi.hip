@@ -32,6 +32,12 @@ extern "C" int bpmd_internal_deflate_keyed(const uint8_t* in, const uint64_t* in
                                            uint32_t* out_len, int32_t* status, int level, int window_bits,
                                            int strategy, const uint32_t* mask_key, hipStream_t stream);
 
+extern "C" int bpmd_internal_deflate_exact(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                           uint32_t n, uint8_t* out, const uint64_t* out_off,
+                                           const uint32_t* out_cap, uint32_t* out_len, int32_t* status, int level,
+                                           int window_bits, int mem_level, int strategy, const uint32_t* mask_key,
+                                           hipStream_t stream);
+
 extern "C" int bpmd_internal_deflate_takeover(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                               uint32_t n, uint8_t* out, const uint64_t* out_off,
                                               const uint32_t* out_cap, uint32_t* out_len, int32_t* status, int level,
@@ -87,7 +93,8 @@ uint8_t* scratch_for(hipStream_t s, size_t bytes, int which = 0)
 }
 }
 
-// scratch block `which` (0 inflate queue, 1-2 deflate workspace) for other
+// scratch block `which` (0 inflate queue, 1-2 deflate workspace, 3-4 exact
+// deflate queue and workspace) for other
 // translation units
 extern "C" void* bpmd_internal_scratch(hipStream_t s, size_t bytes, int which)
 {
@@ -228,6 +235,15 @@ int deflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
         return BPMD_R_INVALID_ARGUMENT;
     int r = bpmd_init();
     if (r) return r;
+    if (cfg->flags & BPMD_F_EXACT) {
+        // the reference's own algorithm, message by message (pmd_deflate_exact.hip)
+        if (hist) return BPMD_R_INVALID_ARGUMENT;
+        return bpmd_internal_deflate_exact(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
+                                           d_status, level, wbits, cfg->mem_level, cfg->strategy, key,
+                                           (hipStream_t)stream)
+                   ? BPMD_R_HIP_ERROR
+                   : BPMD_R_OK;
+    }
     int e = hist ? bpmd_internal_deflate_takeover(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap,
                                                   d_out_len, d_status, level, wbits, cfg->strategy, hist,
                                                   (hipStream_t)stream)

@@ -29,6 +29,7 @@ ERRORS = ("ok", "need_buffers", "end_of_stream", "need_dict", "stream_error", "i
           "missing_eob", "invalid_literal_length", "invalid_distance_code", "invalid_distance",
           "over_subscribed_length", "incomplete_length_set", "general")
 F_RAW = 1
+F_EXACT = 2   # deflate: bit-identical to Beast (BPMD_F_EXACT)
 # utf8_checker verdicts (bpmd_utf8) and websocket::error::bad_frame_payload
 UTF8_VALID, UTF8_INCOMPLETE, UTF8_INVALID = 0, 1, 2
 BAD_FRAME_PAYLOAD = 256
@@ -189,11 +190,12 @@ def inflate_batch(src: Batch, out_cap, window_bits: int = 15, raw: bool = False,
 
 def deflate_batch(src: Batch, level: int = 6, window_bits: int = 15, mem_level: int = 4, strategy: int = 0,
                   stream=None, out_cap=None, out: torch.Tensor | None = None,
-                  out_off: torch.Tensor | None = None) -> Result:
+                  out_off: torch.Tensor | None = None, exact: bool = False) -> Result:
     """Deflate every message of `src` into a permessage-deflate payload
     (tail stripped) on the current GPU, asynchronous on `stream`.
 
     Slots default to deflate_upper_bound(len) bytes, which always suffices.
+    exact=True (BPMD_F_EXACT): payloads bit-identical to Beast's deflater.
     """
     L = lib()
     dev = src.data.device
@@ -212,7 +214,7 @@ def deflate_batch(src: Batch, level: int = 6, window_bits: int = 15, mem_level: 
         out = torch.empty(total + 16, dtype=torch.uint8, device=dev)
     out_len = torch.empty(n, dtype=torch.int32, device=dev)
     status = torch.empty(n, dtype=torch.int32, device=dev)
-    cfg = _Cfg(level, window_bits, mem_level, strategy, 0)
+    cfg = _Cfg(level, window_bits, mem_level, strategy, F_EXACT if exact else 0)
     _check(L.bpmd_deflate_batch(ctypes.byref(cfg), _ptr(src.data), _ptr(src.off), _ptr(src.len), n, _ptr(out),
                                 _ptr(out_off), _ptr(cap), _ptr(out_len), _ptr(status), _stream_handle(stream)),
            "bpmd_deflate_batch")
@@ -303,7 +305,7 @@ def read_batch(src: Batch, out_cap, key=None, text=None, window_bits: int = 15, 
 
 def write_batch(src: Batch, key=None, level: int = 6, window_bits: int = 15, mem_level: int = 4, strategy: int = 0,
                 stream=None, out_cap=None, out: torch.Tensor | None = None,
-                out_off: torch.Tensor | None = None) -> Result:
+                out_off: torch.Tensor | None = None, exact: bool = False) -> Result:
     """Send path, fused (write.hpp:655-703): deflate_batch with each payload
     masked by `key` in the kernel's output stores (client role)."""
     L = lib()
@@ -316,7 +318,7 @@ def write_batch(src: Batch, key=None, level: int = 6, window_bits: int = 15, mem
     k = _keys(key, n, dev)
     out_len = torch.empty(n, dtype=torch.int32, device=dev)
     status = torch.empty(n, dtype=torch.int32, device=dev)
-    cfg = _Cfg(level, window_bits, mem_level, strategy, 0)
+    cfg = _Cfg(level, window_bits, mem_level, strategy, F_EXACT if exact else 0)
     _check(L.bpmd_write_batch(ctypes.byref(cfg), _ptr(src.data), _ptr(src.off), _ptr(src.len), _optr(k), n,
                               _ptr(out), _ptr(out_off), _ptr(cap), _ptr(out_len), _ptr(status),
                               _stream_handle(stream)), "bpmd_write_batch")

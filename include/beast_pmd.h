@@ -66,6 +66,9 @@ enum bpmd_strategy {
 
 /* flags */
 #define BPMD_F_RAW 1u   /* inflate: plain inflate_stream::write() semantics, no 00 00 FF FF tail */
+#define BPMD_F_EXACT 2u /* deflate: payloads bit-identical to Beast's deflate_stream (the
+                           reference's parse, block splits and trees; slower). Not with
+                           context takeover. */
 
 /* Codec configuration: the subset of websocket::permessage_deflate
  * (websocket/option.hpp:34-67) that reaches the codec after negotiation
