@@ -163,23 +163,16 @@ struct Cfg {
     uint32_t wbits, hbits, lit_bufsize;
 };
 
-// one message's deflater (the fields of detail::deflate_stream this path uses)
-struct Dx {
+// one block's Huffman coding and bit emission (tr_flush_block and below),
+// called when the symbol buffer fills or a flush ends: out of line, on a
+// private copy, so the parser's state stays in registers
+struct Blk {
     Trees* T;
-    uint8_t* win;
-    uint16_t* prv;
-    uint16_t* hd;
     uint8_t* syms;
-    const uint8_t* msg;
-    uint32_t len, in_pos;
-    uint32_t wsize, wmask, window_size, hash_size, hash_mask, hash_shift, maxdist;
-    int level, strategy, parser;
-    Lvl L;
-    uint32_t strstart, lookahead, insert, ins_h, high_water;
+    const uint8_t* win;
+    int level, strategy;
+    uint32_t sym_next;
     int32_t block_start;
-    uint32_t prev_length, match_length, prev_match, match_start;
-    bool match_available;
-    uint32_t sym_next, sym_end, lit_bufsize;
     uint32_t opt_len, static_len;
     Bits bw;
     TDesc ld, dd, bd;
@@ -194,7 +187,6 @@ struct Dx {
         if (lane_id() == 0) T->lt[EOBS].f = 1;
         mem_fence();
         opt_len = static_len = 0;
-        sym_next = 0;
     }
     __device__ uint32_t stat_len(const TDesc& d, int n) const { return d.kind == 0 ? fix_llen(n) : 5u; }
     __device__ uint32_t xbits(const TDesc& d, int n) const
@@ -460,7 +452,7 @@ struct Dx {
         bw.opos += n;
     }
     // tr_flush_block (deflate_stream.ipp:1425-1518)
-    __device__ void close_block(bool has_buf, uint32_t stored_len, bool last)
+    __device__ __forceinline__ void close_inline(bool has_buf, uint32_t stored_len, bool last)
     {
         uint32_t opt_lenb, static_lenb;
         int max_blindex = 0;
@@ -495,9 +487,39 @@ struct Dx {
         reset_block();
         if (last) bw.windup();
     }
+    __device__ __attribute__((noinline)) void close_block(bool has_buf, uint32_t stored_len, bool last)
+    {
+        Blk L = *this;
+        L.close_inline(has_buf, stored_len, last);
+        *this = L;
+    }
+};
+
+// one message's deflater (the fields of detail::deflate_stream this path uses)
+struct Dx {
+    Trees* T;
+    uint8_t* win;
+    uint16_t* prv;
+    uint16_t* hd;
+    uint8_t* syms;
+    const uint8_t* msg;
+    uint32_t len, in_pos;
+    uint32_t wsize, wmask, window_size, hash_size, hash_mask, hash_shift, maxdist;
+    int level, strategy, parser;
+    Lvl L;
+    uint32_t strstart, lookahead, insert, ins_h, high_water;
+    int32_t block_start;
+    uint32_t prev_length, match_length, prev_match, match_start;
+    bool match_available;
+    uint32_t sym_next, sym_end, lit_bufsize;
+    Blk* B;
+
     __device__ void flush_block(bool last)
     {
-        close_block(block_start >= 0, (uint32_t)((int32_t)strstart - block_start), last);
+        B->sym_next = sym_next;
+        B->block_start = block_start;
+        B->close_block(block_start >= 0, (uint32_t)((int32_t)strstart - block_start), last);
+        sym_next = 0;
         block_start = (int32_t)strstart;
     }
     __device__ bool tally_lit(uint32_t c)
@@ -847,7 +869,23 @@ struct Dx {
 __device__ int32_t exact_msg(Trees* T, uint8_t* win, uint16_t* prv, uint16_t* hd, uint8_t* syms, uint32_t prv_n,
                              const uint8_t* msg, uint32_t len, uint8_t* out, uint32_t cap, const Cfg& c)
 {
+    Blk b;
+    b.T = T;
+    b.syms = syms;
+    b.win = win;
+    b.level = c.level;
+    b.strategy = c.strategy;
+    b.ld = TDesc{T->lt, 0, NLC, MAXB, 0};
+    b.dd = TDesc{T->dt, 1, NDC, MAXB, 0};
+    b.bd = TDesc{T->bt, 2, NBL, MAXBL, 0};
+    b.bw.out = out;
+    b.bw.cap = cap;
+    b.bw.acc = 0;
+    b.bw.nacc = 0;
+    b.bw.opos = 0;
+    b.reset_block();
     Dx s;
+    s.B = &b;
     s.T = T;
     s.win = win;
     s.prv = prv;
@@ -869,20 +907,12 @@ __device__ int32_t exact_msg(Trees* T, uint8_t* win, uint16_t* prv, uint16_t* hd
     s.parser = s.L.parser;
     s.lit_bufsize = c.lit_bufsize;
     s.sym_end = (c.lit_bufsize - 1) * 3;
-    s.ld = TDesc{T->lt, 0, NLC, MAXB, 0};
-    s.dd = TDesc{T->dt, 1, NDC, MAXB, 0};
-    s.bd = TDesc{T->bt, 2, NBL, MAXBL, 0};
-    s.bw.out = out;
-    s.bw.cap = cap;
-    s.bw.acc = 0;
-    s.bw.nacc = 0;
-    s.bw.opos = 0;
+    s.sym_next = 0;
     // init / lm_init (deflate_stream.ipp:595-718): prev_ and head cleared
     for (uint32_t j = lane_id(); j < prv_n; j += WAVE) prv[j] = 0;
     for (uint32_t j = lane_id(); j < s.hash_size; j += WAVE) hd[j] = 0;
     mem_fence();
     s.high_water = 0;
-    s.reset_block();
     s.strstart = 0;
     s.block_start = 0;
     s.lookahead = 0;
@@ -891,21 +921,21 @@ __device__ int32_t exact_msg(Trees* T, uint8_t* win, uint16_t* prv, uint16_t* hd
     s.match_available = false;
     s.match_start = s.prev_match = 0;
     s.ins_h = 0;
-    // write(Flush::none) over the message (skipped for an empty one), then the
-    // reference's checks: input left or no room -> need_buffers
-    if (len) {
-        s.run(FL_NONE);
-        if (s.bw.bytes_done() >= cap) return -1;
+    // write(Flush::none) over the message (skipped for an empty one), then
+    // write(Flush::block), then write(Flush::sync), with the reference's
+    // checks after each: input left or no room after Flush::none, fewer than
+    // 6 bytes of room after Flush::block -> need_buffers.  (One call site of
+    // the parsers, so they are inlined once.)
+    for (int ph = len ? 0 : 1; ph < 3; ++ph) {
+        s.run(ph == 0 ? FL_NONE : ph == 1 ? FL_BLOCK : FL_SYNC);
+        if (ph == 0 && b.bw.bytes_done() >= cap) return -1;
+        if (ph == 1 && b.bw.bytes_done() + 6 > cap) return -1;
     }
-    // write(Flush::block); then at least 6 bytes of room for Flush::sync
-    s.run(FL_BLOCK);
-    if (s.bw.bytes_done() + 6 > cap) return -1;
-    // write(Flush::sync): the parser finds no input and emits nothing; the
-    // empty stored block's header bits + pad stay, its 00 00 FF FF is dropped
-    s.run(FL_SYNC);
-    s.bw.put(0, 3);
-    s.bw.windup();
-    return (int32_t)s.bw.opos;
+    // Flush::sync's parser found no input and emitted nothing; the empty
+    // stored block's header bits + pad stay, its 00 00 FF FF is dropped
+    b.bw.put(0, 3);
+    b.bw.windup();
+    return (int32_t)b.bw.opos;
 }
 
 constexpr uint32_t SMALL_MAX = 8192 - LOOK;   // messages the LDS kernel takes
