@@ -310,6 +310,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--msgs", type=int, default=N_MSGS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-exact", action="store_true", help="skip the exact-mode (BPMD_F_EXACT) deflate leg")
     ap.add_argument("--no-deflate", action="store_true")
     ap.add_argument("--no-frame", action="store_true")
     ap.add_argument("--no-mixed", action="store_true")
@@ -492,6 +493,22 @@ def main():
                          "unit": "GB/s", "frac": round(dalg / (d_kern * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
                          "kernel": "deflate_kernel", "kernel_ms": round(d_kern, 4), "alg_bytes_per_launch": dalg},
         }
+        exact_len = None
+        if not args.no_exact:
+            # BPMD_F_EXACT: the reference's own parse, blocks and trees, bit for bit
+            def exact_step():
+                return pmd.deflate_batch(src3, level=6, mem_level=4, out_cap=cap3, out=out3, out_off=off3o, exact=True)
+
+            ex = exact_step()
+            torch.cuda.synchronize()
+            exact_len = ex.out.len.cpu().numpy().astype(np.int64)
+            e_ok = int((ex.status != 0).sum()) == 0
+            e_step, _ = timer.run(exact_step, min(args.steps, 3), 1)
+            result["deflate"]["exact"] = {
+                "deflate_value": round(uncomp * world / (1 << 30) / e_step, 3),
+                "ms_per_step": round(e_step * 1e3, 3), "ratio": round(int(exact_len.sum()) / uncomp, 4),
+                "status_ok": bool(e_ok), "steps": min(args.steps, 3),
+                "mode": "BPMD_F_EXACT (bit-identical to Beast's deflate_stream; tests/test_gpu_deflate_exact.py)"}
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baselines(comp_buf, comp_off, comp_len, raw_len.astype(np.uint32), raw3, off3, len3)
             dcpu = cpu["deflate"]
@@ -499,6 +516,8 @@ def main():
             if beast_len is not None:
                 k = len(beast_len)
                 result["deflate"]["size_vs_beast"] = round(float(gpu_len[:k].sum()) / float(beast_len.sum()), 4)
+                if exact_len is not None:
+                    result["deflate"]["exact"]["same_size_as_beast"] = f"{int((exact_len[:k] == beast_len).sum())}/{k}"
                 result["deflate"]["size_sample"] = f"first {k} messages, Σ GPU bytes / Σ Beast bytes at L6/mem4"
             if "port" in dcpu:
                 T = cpu["threads"]
