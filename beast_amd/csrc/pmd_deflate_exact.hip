@@ -15,9 +15,9 @@
 // bulk work inside it: the 256-byte match comparisons of longest_match
 // (64 bytes per step, first mismatch by ballot), window fills and slides,
 // table clears.  The window / prev / head arrays live in LDS for messages
-// up to SMALL_MAX bytes at memLevel <= 5 (SMALL kernel) and in a per-wave
-// global workspace otherwise; the code is the same through generic
-// pointers.  Tree construction uses per-wave LDS in both kernels.
+// of up to 4 KiB and up to 8 KiB at memLevel <= 5 (tiers 0 and 1) and in a
+// per-wave global workspace otherwise (tier 2); the code is the same
+// through generic pointers.  Tree construction uses per-wave LDS in all.
 //
 // Reference map: level table deflate_stream.hpp:571-590; reset / init
 // deflate_stream.ipp:227-265, 595-737; fill_window 1520-1669; longest_match
@@ -938,13 +938,21 @@ __device__ int32_t exact_msg(Trees* T, uint8_t* win, uint16_t* prv, uint16_t* hd
     return (int32_t)b.bw.opos;
 }
 
-constexpr uint32_t SMALL_MAX = 8192 - LOOK;   // messages the LDS kernel takes
-constexpr uint32_t SMALL_WIN = 8192 + 512;     // window bytes in LDS
-constexpr uint32_t SMALL_PRV = 8192;           // prev_ entries in LDS
+// LDS tiers by message length (memLevel <= 5): window bytes, prev_ entries.
+// A tier's window holds the whole physical window (2^(windowBits+1)) or, when
+// that is larger, the message plus the reference's look-ahead: then no slide
+// can happen (it needs strstart >= 2 * w_size - 262), and no position reaches
+// past the prev_ entries.  TIER 0: <= 4 KiB (6 waves per CU at memLevel 4),
+// TIER 1: <= 8 KiB - 262, TIER 2: the per-wave global workspace.
+template <int TIER> struct Tier;
+template <> struct Tier<0> { static constexpr uint32_t MAX = 4096, WIN = 4096 + 512, PRV = 4096; };
+template <> struct Tier<1> { static constexpr uint32_t MAX = 8192 - LOOK, WIN = 8192 + 512, PRV = 8192; };
+__host__ __device__ constexpr int tier_of(uint32_t len, uint32_t hbits)
+{
+    return hbits > 12 ? 2 : len <= Tier<0>::MAX ? 0 : len <= Tier<1>::MAX ? 1 : 2;
+}
 
-// SMALL: window / prev / head / symbols in LDS (memLevel <= 5, messages of at
-// most SMALL_MAX bytes); otherwise in the per-wave global workspace ws.
-template <bool SMALL>
+template <int TIER>
 __global__ void __launch_bounds__(64)
 deflate_exact_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                      const uint32_t* __restrict__ in_len, uint32_t n, uint8_t* __restrict__ out,
@@ -958,13 +966,13 @@ deflate_exact_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict_
     uint8_t *win, *syms;
     uint16_t *prv, *hd;
     uint32_t prv_n;
-    if (SMALL) {
+    if constexpr (TIER < 2) {
         uint8_t* p = smem + ((sizeof(Trees) + 15) & ~(size_t)15);
         win = p;
-        p += SMALL_WIN;
+        p += Tier<TIER>::WIN;
         prv = (uint16_t*)p;
-        prv_n = wsize < SMALL_PRV ? wsize : SMALL_PRV;
-        p += 2 * SMALL_PRV;
+        prv_n = wsize < Tier<TIER>::PRV ? wsize : Tier<TIER>::PRV;
+        p += 2 * Tier<TIER>::PRV;
         hd = (uint16_t*)p;
         p += 2 * hash_size;
         syms = p;
@@ -984,7 +992,7 @@ deflate_exact_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict_
     // each kernel leaves the other's messages
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
         const uint32_t len = in_len[i];
-        if (SMALL != (len <= SMALL_MAX && c.hbits <= 12)) continue;
+        if (tier_of(len, c.hbits) != TIER) continue;
         uint8_t* o = out + out_off[i];
         const uint32_t cap = out_cap[i];
         const int32_t r = exact_msg(T, win, prv, hd, syms, prv_n, in + in_off[i], len, o, cap, c);
@@ -1028,10 +1036,14 @@ extern "C" int bpmd_internal_deflate_exact(const uint8_t* in, const uint64_t* in
     hipError_t e;
     const size_t trees = (sizeof(Trees) + 15) & ~(size_t)15;
     if (c.hbits <= 12) {
-        const size_t lds = trees + SMALL_WIN + 2 * SMALL_PRV + 2 * ((size_t)1 << c.hbits) +
-                           3 * (size_t)c.lit_bufsize;
-        hipLaunchKernelGGL(deflate_exact_kernel<true>, dim3(n), dim3(64), lds, stream, in, in_off, in_len, n, out,
-                           out_off, out_cap, out_len, status, mask_key, c, (uint8_t*)nullptr, (size_t)0);
+        const size_t tail = 2 * ((size_t)1 << c.hbits) + 3 * (size_t)c.lit_bufsize;
+        hipLaunchKernelGGL(deflate_exact_kernel<0>, dim3(n), dim3(64), trees + Tier<0>::WIN + 2 * Tier<0>::PRV + tail,
+                           stream, in, in_off, in_len, n, out, out_off, out_cap, out_len, status, mask_key, c,
+                           (uint8_t*)nullptr, (size_t)0);
+        if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+        hipLaunchKernelGGL(deflate_exact_kernel<1>, dim3(n), dim3(64), trees + Tier<1>::WIN + 2 * Tier<1>::PRV + tail,
+                           stream, in, in_off, in_len, n, out, out_off, out_cap, out_len, status, mask_key, c,
+                           (uint8_t*)nullptr, (size_t)0);
         if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     }
     // the rest: window / prev / head / symbols in a per-wave workspace
@@ -1041,7 +1053,7 @@ extern "C" int bpmd_internal_deflate_exact(const uint8_t* in, const uint64_t* in
     const unsigned grid = (unsigned)cus * 4u;
     uint8_t* ws = (uint8_t*)bpmd_internal_scratch(stream, per * grid, 4);
     if (!ws) return (int)hipErrorOutOfMemory;
-    hipLaunchKernelGGL(deflate_exact_kernel<false>, dim3(grid < n ? grid : n), dim3(64), trees, stream, in, in_off,
+    hipLaunchKernelGGL(deflate_exact_kernel<2>, dim3(grid < n ? grid : n), dim3(64), trees, stream, in, in_off,
                        in_len, n, out, out_off, out_cap, out_len, status, mask_key, c, ws, per);
     return (int)hipGetLastError();
 }

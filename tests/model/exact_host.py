@@ -75,7 +75,7 @@ def build():
     if os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(KSRC), os.path.getmtime(__file__)):
         return LIB
     src = open(KSRC).read()
-    body = src[:src.index("constexpr uint32_t SMALL_MAX")]
+    body = src[:src.index("// LDS tiers by message length")]
     body = body.replace('#include "pmd_common.h"', "")
     with open(GEN, "w") as f:
         f.write(SHIM + body + DRIVER)
