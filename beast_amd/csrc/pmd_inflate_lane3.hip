@@ -142,48 +142,6 @@ __device__ __forceinline__ Sym canon_decode(const uint32_t (&Q)[NB], uint32_t c)
     return r;
 }
 
-// The same search over a fixed sub-range of code lengths, [A + 1, A + K]:
-// exact when every code length of the table lies in it (words for shorter
-// lengths never win the min, words for longer ones lose to the longest used
-// length's), with fewer subtractions and mins per symbol.
-template <int A, int K>
-__device__ __forceinline__ Sym canon_decode_sub(const uint32_t (&Q)[15], uint32_t c)
-{
-    const uint32_t k1 = (c + 1) << 15;
-    uint32_t m = Q[A] - k1;
-#pragma unroll
-    for (int i = A + 1; i + 1 < A + K; i += 2) {
-        const uint32_t x = Q[i] - k1, y = Q[i + 1] - k1;
-        m = __builtin_elementwise_min(m, __builtin_elementwise_min(x, y));
-    }
-    if (K % 2 == 0) m = __builtin_elementwise_min(m, Q[A + K - 1] - k1);
-    Sym r;
-    r.inval = (m >> 31) != 0;
-    const uint32_t q = m + ((c + 1) << 15);
-    r.L = (q >> 11) & 15u;
-    const int32_t below = (int32_t)(c - (q >> 15)) >> (15 - (int32_t)r.L);
-    r.idx = r.inval ? 0u : (uint32_t)((int32_t)(q & 0x7ffu) + below);
-    return r;
-}
-// literal/length codes of lengths 4..14 and distance codes of lengths 1..10
-// (the common case of dynamic blocks, and the fixed tables)
-template <bool F>
-__device__ __forceinline__ Sym dec_lit(const uint32_t (&Q)[15], uint32_t c)
-{
-    if constexpr (F) return canon_decode_sub<3, 11>(Q, c);
-    else return canon_decode<15>(Q, c);
-}
-template <bool F>
-__device__ __forceinline__ Sym dec_dist(const uint32_t (&Q)[15], uint32_t c)
-{
-    if constexpr (F) return canon_decode_sub<0, 10>(Q, c);
-    else return canon_decode<15>(Q, c);
-}
-template <bool B>
-struct BoolTag {
-    static constexpr bool value = B;
-};
-
 // The reference's slow path asks for the root bits, or for root + sub-table
 // index bits when the code is longer than the root: a sub-table covers one
 // root prefix and is as deep as the longest code under it, i.e. the length
@@ -619,7 +577,6 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
     uint32_t pos = 0, head = 0;
     Canon<15> tl, td;
     Canon<7> tc;
-    bool sub_ok = true;   // the tables' code lengths fit dec_lit / dec_dist's sub-ranges
     // header state
     uint32_t nlen = 0, ndist = 0, want = 0, have = 0, prev = 0;
     bool eob_seen = false, cl_empty = false;
@@ -731,11 +688,7 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
         const uint32_t st0 = st;
         const uint32_t head0 = head;
         L3_LAP(0);
-        // every lane's tables within the sub-ranges: the cheaper searches (one
-        // wave-uniform branch between two copies of the data step)
-        const bool sub = __ballot(st == S_DATA && room && !sub_ok) == 0;
-        auto data_step = [&](auto tag) {
-            constexpr bool FAST = decltype(tag)::value;
+        if (st == S_DATA && room) {
             // Up to KLIT symbols per iteration: while there is room for them
             // (input for KLIT - 1 literals plus a whole token, output for KLIT
             // literals, so no event can occur among them) leading literals are
@@ -752,7 +705,7 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
 #pragma unroll
             for (int k = 0; k < KLIT; ++k) {
                 kc[k] = rev15(w >> kp[k]);
-                const Sym y = dec_lit<FAST>(tl.Q, kc[k]);
+                const Sym y = canon_decode<15>(tl.Q, kc[k]);
                 kL[k] = y.L;
                 kx[k] = y.idx;
                 kinv[k] = y.inval;
@@ -818,7 +771,7 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
             len += (uint32_t)(w2 >> L) & lowmask(xl);
             const uint32_t used = L + (is_len ? xl : 0u);
             const uint32_t d15 = rev15(w2 >> used);
-            const Sym yd = dec_dist<FAST>(td.Q, d15);
+            const Sym yd = canon_decode<15>(td.Q, d15);
             const uint32_t Ld = yd.L;
             const uint32_t dsym = T[O_DST + yd.idx];
             const bool invd = yd.inval || dsym >= 30;
@@ -859,10 +812,6 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
             enl = emit && !is_match ? 1u : enl;
             elit = emit && !is_match ? sym : elit;
             pos += emit ? olen : 0u;
-                };
-        if (st == S_DATA && room) {
-            if (sub) data_step(BoolTag<true>{});
-            else data_step(BoolTag<false>{});
         }
 
 
@@ -922,7 +871,6 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
                         }
                         tl.root = 9;
                         td.root = 5;
-                        sub_ok = true;
                         st = S_DATA;
                     } else if (type == 2) {
                         st = S_DYN;
@@ -1155,12 +1103,10 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
 #pragma unroll
                 for (int l = 1; l < 16; ++l) c[l] = h[l] & 0x3ffu;
                 int e = make_canon<15>(c, 9, 1, tl);
-                sub_ok = (c[1] | c[2] | c[3] | c[15]) == 0;
                 if (!e) {
 #pragma unroll
                     for (int l = 1; l < 16; ++l) c[l] = (h[l] >> 20) & 0x3ffu;
                     e = make_canon<15>(c, 6, 2, td);
-                    sub_ok = sub_ok && (c[11] | c[12] | c[13] | c[14] | c[15]) == 0;
                 }
                 if (e) {
                     result = e;
