@@ -27,6 +27,7 @@ extern "C" int bpmd_internal_inflate_lane3(const uint8_t* in, const uint64_t* in
                                            const uint32_t* hist_len, uint32_t hist_max, uint32_t max_in,
                                            const uint32_t* order, uint32_t* qctr, uint32_t grid_wgs,
                                            hipStream_t stream);
+extern "C" const uint32_t* bpmd_internal_lane_order(const uint32_t* in_len, uint32_t n, hipStream_t stream);
 extern "C" int bpmd_internal_deflate_keyed(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                            uint32_t n, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                                            uint32_t* out_len, int32_t* status, int level, int window_bits,
@@ -94,7 +95,7 @@ uint8_t* scratch_for(hipStream_t s, size_t bytes, int which = 0)
 }
 
 // scratch block `which` (0 inflate queue, 1-2 deflate workspace, 3-4 exact
-// deflate queue and workspace) for other
+// deflate queue and workspace, 5 inflate message order) for other
 // translation units
 extern "C" void* bpmd_internal_scratch(hipStream_t s, size_t bytes, int which)
 {
@@ -203,12 +204,20 @@ int inflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
         }();
         if (q_override) wgs = q_override;
         uint32_t* qctr = nullptr;
+        const uint32_t* order = nullptr;
         if (n_msgs > wgs * 64u && !split) {
             qctr = (uint32_t*)scratch_for(s, 256);
             if (!qctr || hipMemsetAsync(qctr, 0, sizeof(uint32_t), s) != hipSuccess) return BPMD_R_HIP_ERROR;
+            // longest first, so no lane starts a long message as the batch drains
+            // (BPMD_INFLATE_ORDER=0: batch order)
+            static const bool ordered = [] {
+                const char* e = getenv("BPMD_INFLATE_ORDER");
+                return !(e && e[0] == '0');
+            }();
+            if (ordered && !(order = bpmd_internal_lane_order(d_in_len, n_msgs, s))) return BPMD_R_HIP_ERROR;
         }
         e = bpmd_internal_inflate_lane3(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
-                                        d_status, raw, key, hist, 1u << cfg->window_bits, split, nullptr, qctr, wgs,
+                                        d_status, raw, key, hist, 1u << cfg->window_bits, split, order, qctr, wgs,
                                         s);
     }
     if (!e && (!lane || split))

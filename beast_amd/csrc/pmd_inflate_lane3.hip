@@ -38,6 +38,8 @@
 // Token word 1: bits 0-2 literal count, 3-11 match length (0 = none),
 // 12-27 distance; bit 31 = END (word 0 = out_len, bits 0-7 = status).
 // Output semantics per message are those of pmd_inflate.hip.
+#include <hipcub/hipcub.hpp>
+
 #include "pmd_common.h"
 
 namespace bpmd {
@@ -1248,6 +1250,52 @@ extern "C" int bpmd_internal_inflate_lane3(const uint8_t* in, const uint64_t* in
     hipLaunchKernelGGL(inflate_lane3_kernel, dim3(grid), dim3(128), WG_MSGS * STRIDE, stream, in, in_off, in_len, n,
                        out, out_off, out_cap, out_len, status, raw, mask_key, hist_len, hist_max, max_in, order, qctr);
     return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------- order
+// Work-queue batches of mixed sizes (configs[3]): lanes take messages
+// longest compressed payload first, so the long messages start while the
+// short ones still fill the lanes that finish early, and no lane starts a
+// 64 KiB message as the batch drains.  Keys are in_len >> 6 (coarse classes
+// are enough for balance, and fewer radix passes), stable in message order.
+namespace bpmd {
+namespace lp3 {
+__global__ void __launch_bounds__(256) order_keys_kernel(const uint32_t* __restrict__ in_len, uint32_t n,
+                                                         uint32_t* __restrict__ key, uint32_t* __restrict__ idx)
+{
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < n) {
+        key[i] = in_len[i] >> 6;
+        idx[i] = i;
+    }
+}
+}  // namespace lp3
+}  // namespace bpmd
+
+extern "C" void* bpmd_internal_scratch(hipStream_t s, size_t bytes, int which);
+
+// order[0, n) = message indices, longest payload first; returns null on error
+extern "C" const uint32_t* bpmd_internal_lane_order(const uint32_t* in_len, uint32_t n, hipStream_t stream)
+{
+    size_t temp = 0;
+    if (hipcub::DeviceRadixSort::SortPairsDescending(nullptr, temp, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                                     (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, 26,
+                                                     stream) != hipSuccess)
+        return nullptr;
+    const size_t words = (size_t)n * 4;   // key in, key out, index in, index out
+    uint8_t* p = (uint8_t*)bpmd_internal_scratch(stream, words * 4 + temp + 256, 5);
+    if (!p) return nullptr;
+    uint32_t* kin = (uint32_t*)p;
+    uint32_t* kout = kin + n;
+    uint32_t* iin = kout + n;
+    uint32_t* iout = iin + n;
+    void* tmp = (void*)(((uintptr_t)(iout + n) + 255) & ~(uintptr_t)255);
+    hipLaunchKernelGGL(bpmd::lp3::order_keys_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, in_len, n, kin, iin);
+    if (hipGetLastError() != hipSuccess) return nullptr;
+    if (hipcub::DeviceRadixSort::SortPairsDescending(tmp, temp, kin, kout, iin, iout, (int)n, 0, 26, stream) !=
+        hipSuccess)
+        return nullptr;
+    return iout;
 }
 
 // diagnostic counters of the pipelined lane kernel (meaningful only in the -DBPMD_PROF build)
