@@ -284,60 +284,120 @@ __device__ __forceinline__ void merge_tree(HuffLds& H, unsigned kb, unsigned m, 
     }
 }
 
-// Serial build for a tiny alphabet (the code-length code, 19 symbols) on
-// lane 0, same algorithm as lz::huff_lengths_host.
-__device__ __forceinline__ void tiny_lengths(const uint32_t* freq, unsigned n, unsigned max_bits, uint8_t* lens,
-                                             uint32_t* key, uint16_t* iw, uint16_t* parent, uint8_t* depth)
+// The code-length code (19 symbols, lengths <= 7): Huffman lengths as
+// lz::huff_lengths_host computes them, then canonical codes, the count of
+// code-length code lengths sent (HCLEN + 4) and the dynamic header's size
+// (deflate_stream.ipp:1396-1418 build_bl_tree, 1420-1438 send_all_trees).
+// Wave-parallel: symbol s in lane s, ranks by comparing each key with every
+// other key, the 18-step merge and the depths as wave-uniform loops over
+// v_readlane (no LDS round trip per step).
+__device__ void bl_tree_wave(HuffLds& H, uint32_t& hdr_bits, uint32_t& nbl_out)
 {
-    uint32_t f2[lz::N_BLCODES];
-    unsigned used = 0;
-    for (unsigned i = 0; i < n; ++i) { f2[i] = freq[i]; lens[i] = 0; used += f2[i] != 0; }
-    for (unsigned i = 0; used < 2 && i < n; ++i)
-        if (f2[i] == 0) { f2[i] = 1; ++used; }
-    unsigned m = 0;
-    for (unsigned i = 0; i < n; ++i)
-        if (f2[i]) {
-            const uint32_t v = (f2[i] << 9) | i;
-            unsigned j = m++;
-            while (j > 0 && key[j - 1] > v) { key[j] = key[j - 1]; --j; }
-            key[j] = v;
-        }
-    unsigned li = 0, ii = 0;
-    for (unsigned k = 0; k + 1 < m; ++k) {
-        uint32_t w[2];
-        unsigned id[2];
-        for (int t = 0; t < 2; ++t) {
-            const bool leaf = li < m && (ii >= k || (key[li] >> 9) <= iw[ii]);
-            if (leaf) { w[t] = key[li] >> 9; id[t] = li++; }
-            else { w[t] = iw[ii]; id[t] = m + ii++; }
-        }
-        iw[k] = (uint16_t)(w[0] + w[1]);
-        parent[id[0]] = parent[id[1]] = (uint16_t)(m + k);
+    using namespace lz;
+    const unsigned lane = lane_id();
+    const bool sl = lane < (unsigned)N_BLCODES;
+    const uint32_t f0 = sl ? H.bf[lane] : 0u;
+    // at least two codes: the first unused symbols get frequency 1
+    const unsigned used = (unsigned)__builtin_popcountll(ballot(f0 != 0));
+    const uint64_t zero = ballot(sl && f0 == 0);
+    const uint32_t f = (sl && f0 == 0 && used < 2 && popc_below(zero) < 2 - used) ? 1u : f0;
+    const uint32_t key = f ? (f << 9) | lane : 0xFFFFFFFFu;
+    const unsigned m = (unsigned)__builtin_popcountll(ballot(f != 0));
+    // ascending rank of each used key (keys are distinct)
+    unsigned rank = 0;
+#pragma unroll
+    for (unsigned j = 0; j < (unsigned)N_BLCODES; ++j) {
+        const uint32_t kj = (uint32_t)__builtin_amdgcn_readlane((int)key, (int)j);
+        rank += kj < key ? 1u : 0u;
     }
-    const unsigned root = 2 * m - 2;
-    depth[root] = 0;
-    for (int v = (int)root - 1; v >= 0; --v) depth[v] = (uint8_t)(depth[parent[v]] + 1);
-    unsigned blc[16] = {0};
-    int overflow = 0;
-    for (unsigned i = 0; i < m; ++i) {
-        unsigned d = depth[i];
-        if (d > max_bits) { d = max_bits; ++overflow; }
-        blc[d]++;
+    if (f) H.r.tkey[rank] = key;
+    wave_sync();
+    const uint32_t sorted = lane < m ? H.r.tkey[lane] : 0u;   // lane r: the r-th smallest key
+    const uint32_t sw = sorted >> 9;
+    // two-queue merge (leaves 0..m-1, internal nodes m..2m-2)
+    uint32_t iw = 0, par = 0;
+    {
+        unsigned li = 0, ii = 0;
+        uint32_t kw = (uint32_t)__builtin_amdgcn_readlane((int)sw, 0);
+        for (unsigned k = 0; k + 1 < m; ++k) {
+            uint32_t w[2];
+            unsigned id[2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const uint32_t iwv = ii < k ? (uint32_t)__builtin_amdgcn_readlane((int)iw, (int)ii) : 0xFFFFFFFFu;
+                if (li < m && (ii >= k || kw <= iwv)) {
+                    w[t] = kw;
+                    id[t] = li++;
+                    kw = li < m ? (uint32_t)__builtin_amdgcn_readlane((int)sw, (int)li) : 0u;
+                } else {
+                    w[t] = iwv;
+                    id[t] = m + ii++;
+                }
+            }
+            iw = lane == k ? (uint32_t)(uint16_t)(w[0] + w[1]) : iw;
+            par = (lane == id[0] || lane == id[1]) ? m + k : par;
+        }
     }
-    if (overflow) {
-        do {
-            unsigned bits = max_bits - 1;
-            while (blc[bits] == 0) --bits;
-            blc[bits]--;
-            blc[bits + 1] += 2;
-            blc[max_bits]--;
+    // depths top-down (root = 2m - 2; node v's parent is above it)
+    uint32_t dep = 0;
+    for (int v = (int)(2 * m) - 3; v >= 0; --v) {
+        const unsigned p = (unsigned)__builtin_amdgcn_readlane((int)par, v);
+        const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)dep, (int)p) + 1u;
+        dep = lane == (unsigned)v ? d : dep;
+    }
+    // length limit (deflate_stream.ipp gen_bitlen): clamp, repair the Kraft
+    // overflow, reassign lengths in frequency order
+    uint32_t len = dep;
+    const uint64_t over_m = ballot(lane < m && dep > (uint32_t)MAX_BL_BITS);
+    if (over_m) {
+        int overflow = (int)__builtin_popcountll(over_m);
+        uint32_t blc = 0;   // lane b: leaves of length b
+#pragma unroll
+        for (unsigned b2 = 1; b2 <= (unsigned)MAX_BL_BITS; ++b2) {
+            const unsigned c = (unsigned)__builtin_popcountll(
+                ballot(lane < m && (dep > (uint32_t)MAX_BL_BITS ? (uint32_t)MAX_BL_BITS : dep) == b2));
+            blc = lane == b2 ? c : blc;
+        }
+        while (overflow > 0) {
+            unsigned bits = MAX_BL_BITS - 1;
+            while (__builtin_amdgcn_readlane((int)blc, (int)bits) == 0) --bits;
+            blc = lane == bits ? blc - 1u : lane == bits + 1 ? blc + 2u : blc;
+            blc = lane == (unsigned)MAX_BL_BITS ? blc - 1u : blc;
             overflow -= 2;
-        } while (overflow > 0);
-        int i = (int)m - 1;
-        for (unsigned bits = 1; bits <= max_bits; ++bits)
-            for (unsigned c = 0; c < blc[bits]; ++c) depth[i--] = (uint8_t)bits;
+        }
+        // the r-th most frequent leaf (leaf m - 1 - r) gets the r-th shortest length
+        const unsigned r = m - 1 - lane;
+        unsigned cum = 0, bits = MAX_BL_BITS;
+        for (unsigned b2 = MAX_BL_BITS; b2 >= 1; --b2) {
+            cum = 0;
+            for (unsigned b3 = 1; b3 <= b2; ++b3) cum += (uint32_t)__builtin_amdgcn_readlane((int)blc, (int)b3);
+            if (r < cum) bits = b2;
+        }
+        len = bits;
     }
-    for (unsigned i = 0; i < m; ++i) lens[key[i] & 511] = depth[i];
+    // lengths by symbol
+    if (sl) H.bll[lane] = 0;
+    wave_sync();
+    if (lane < m) H.bll[sorted & 511] = (uint8_t)len;
+    wave_sync();
+    const uint32_t bl = sl ? H.bll[lane] : 0u;
+    // canonical codes: next_code per length, then rank among equal lengths by symbol
+    uint32_t code = 0, next = 0;
+#pragma unroll
+    for (unsigned b2 = 1; b2 <= (unsigned)MAX_BL_BITS; ++b2) {
+        const uint64_t mb = ballot(sl && bl == b2);
+        if (bl == b2) code = next + popc_below(mb);
+        next = (next + (uint32_t)__builtin_popcountll(mb)) << 1;
+    }
+    if (sl) H.blc[lane] = bl ? pack_code(code, bl) : 0u;
+    // code lengths sent: down to the last nonzero in bl_order, at least 4
+    const bool nz = sl && H.bll[bl_order(sl ? lane : 0u)] != 0;
+    const uint64_t nzm = ballot(nz);
+    const unsigned nbl = nzm ? 64u - (unsigned)__builtin_clzll(nzm) : 0u;
+    nbl_out = nbl < 4 ? 4u : nbl;
+    const uint32_t xb = lane == 16 ? 2u : lane == 17 ? 3u : lane == 18 ? 7u : 0u;
+    hdr_bits = 3 + 5 + 5 + 4 + 3 * nbl_out + wave_sum(sl ? f0 * (bl + xb) : 0u);
+    wave_sync();
 }
 
 // Lit/len and distance code lengths + canonical codes for the current
@@ -865,23 +925,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
             nrle = run_carry;
             wave_sync();
         }
-        if (lane == 0) {
-            tiny_lengths(H.bf, N_BLCODES, MAX_BL_BITS, H.bll, H.r.tkey, H.iw, H.parent, H.depth);
-            // canonical code-length codes
-            unsigned cntb[8] = {0}, next[8];
-            for (int s = 0; s < N_BLCODES; ++s) cntb[H.bll[s]]++;
-            cntb[0] = 0;
-            unsigned code = 0;
-            for (int b2 = 1; b2 <= MAX_BL_BITS; ++b2) { code = (code + cntb[b2 - 1]) << 1; next[b2] = code; }
-            for (int s = 0; s < N_BLCODES; ++s) H.blc[s] = H.bll[s] ? pack_code(next[H.bll[s]]++, H.bll[s]) : 0;
-            unsigned nbl = N_BLCODES;
-            while (nbl > 4 && H.bll[bl_order(nbl - 1)] == 0) --nbl;
-            uint32_t hb = 3 + 5 + 5 + 4 + 3 * nbl;
-            for (int s = 0; s < N_BLCODES; ++s)
-                hb += H.bf[s] * (H.bll[s] + (s == 16 ? 2u : s == 17 ? 3u : s == 18 ? 7u : 0u));
-            H.misc[0] = hb;
-            H.misc[1] = nbl;
-        }
+        bl_tree_wave(H, hdr_bits, blcodes);
         pf.lap(9);
         uint32_t dyn = 0, fix = 0;
         for (unsigned i = lane; i < N_LCODES; i += WAVE) {
@@ -898,8 +942,6 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
         dyn = wave_sum(dyn);
         fix = wave_sum(fix) + 3;
         wave_sync();
-        hdr_bits = H.misc[0];
-        blcodes = H.misc[1];
         dyn += hdr_bits;
         uint32_t opt_b = (dyn + 7) >> 3;
         const uint32_t fix_b = (fix + 7) >> 3;

@@ -638,6 +638,9 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
     if (valid) begin(m);
     L3_DECL;
     L3_LAPDECL;
+#ifdef BPMD_PROF
+    unsigned long long l3x_[4] = {0, 0, 0, 0};
+#endif
 
     for (;;) {
         if (!exhausted) {
@@ -685,6 +688,14 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
         compiler_fence();
         const bool room = head - taken < RING;
         const bool ring_empty = head == taken;
+#ifdef BPMD_PROF
+        // lane states per iteration: [12] data lanes blocked by a full ring,
+        // [13] data lanes with room, [14] finished lanes, [15] header lanes
+        l3x_[0] += __builtin_popcountll(__ballot(st == S_DATA && !room));
+        l3x_[1] += __builtin_popcountll(__ballot(st == S_DATA && room));
+        l3x_[2] += __builtin_popcountll(__ballot(fin && !send_new));
+        l3x_[3] += __builtin_popcountll(__ballot(st != S_DATA && st != S_DONE));
+#endif
         // this iteration's token
         uint32_t enl = 0, elit = 0, emlen = 0, edist = 0;
         const uint32_t st0 = st;
@@ -1195,6 +1206,10 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
     }
     L3_FLUSH(0);
     L3_LAPFLUSH();
+#ifdef BPMD_PROF
+    if ((threadIdx.x & 63) == 0)
+        for (int i = 0; i < 4; ++i) atomicAdd(&g_l3prof[12 + i], l3x_[i]);
+#endif
 }
 
 // A workgroup is one decoder wave and one expander wave over 64 messages;

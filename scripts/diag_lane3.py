@@ -16,13 +16,14 @@ from beast_amd import pmd, synth  # noqa: E402
 
 
 def main():
-    n = 65536
-    lens = np.full(n, 4096, dtype=np.uint32)
-    raw, off, ln = synth.make_batch("json", lens, seed=0x5EED0002)
+    n = int(os.environ.get("DIAG_MSGS", "65536"))
+    size = int(os.environ.get("DIAG_SIZE", "4096"))
+    lens = np.full(n, size, dtype=np.uint32)
+    raw, off, ln = synth.make_batch(os.environ.get("DIAG_KIND", "json"), lens, seed=0x5EED0002)
     buf, coff, clen = bench.pack(bench.pmd_compress_host(raw, off, ln))
     dev = torch.device("cuda", 0)
     src = pmd.Batch(torch.from_numpy(buf).to(dev), torch.from_numpy(coff).to(dev), torch.from_numpy(clen).to(dev))
-    cap = torch.full((n,), 4096, dtype=torch.int32, device=dev)
+    cap = torch.full((n,), size, dtype=torch.int32, device=dev)
     L = pmd.lib()
     c = (ctypes.c_ulonglong * 16)()
     pmd.inflate_batch(src, cap)
@@ -31,10 +32,11 @@ def main():
     r = pmd.inflate_batch(src, cap)
     torch.cuda.synchronize()
     L.bpmd_diag_lane3_counters(c, 1)
-    ok = torch.equal(r.out.data[: n * 4096].view(n, 4096), torch.from_numpy(raw.reshape(n, 4096)).to(dev))
+    ok = torch.equal(r.out.data[: n * size].view(n, size), torch.from_numpy(raw.reshape(n, size)).to(dev))
     w = n // 64
     names = ["dec cycles", "dec iters", "dec sleeps", "dec hdr iters", "exp cycles", "exp iters", "exp sleeps", "-",
-             "dec lap: input+tail", "dec lap: S_DATA", "dec lap: headers", "dec lap: publish+loop"]
+             "dec lap: input+tail", "dec lap: S_DATA", "dec lap: headers", "dec lap: publish+loop",
+             "lanes: data, ring full", "lanes: data, room", "lanes: finished", "lanes: in headers"]
     for i, nm in enumerate(names):
         if nm == "-":
             continue

@@ -1,0 +1,3 @@
+# lane-kernel role counters on the C5 shape (64 KiB binary, 16 Ki messages), prof build
+set -o pipefail
+BPMD_INFLATE=lane BPMD_LIB=beast_amd/libbeast_pmd_prof.so DIAG_KIND=binary DIAG_SIZE=65536 DIAG_MSGS=16384 timeout -k 10 300 python -u scripts/diag_lane3.py
