@@ -150,6 +150,14 @@ struct Win {
     }
 };
 
+// a wave-uniform value moved into a VGPR (see the parse loop)
+__device__ __forceinline__ unsigned to_vgpr(unsigned x)
+{
+    unsigned v;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "s"(x));
+    return v;
+}
+
 // number of equal leading bytes of two 8-byte groups (8 = all)
 __device__ __forceinline__ unsigned eq_bytes(uint64_t a, uint64_t b)
 {
@@ -708,9 +716,15 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
             // iteration does one unit of work per lane (a parse decision, one
             // chain candidate, or 8 more bytes of a match) -- nested
             // divergent loops would multiply lane imbalance.
-            const bool lazy = P.L.parser == P_SLOW;
-            const bool no_match = P.strategy == 2, rle = P.strategy == 3;
-            const unsigned chain_max = P.chain;
+            // The level's limits are wave-uniform, but kept in VGPRs here: in
+            // scalar registers the loop's many lane masks push them out to
+            // VGPR lanes, reloaded (v_readlane) every iteration.
+            const unsigned max_dist = to_vgpr(P.max_dist), good = to_vgpr(P.L.good), nice_l = to_vgpr(P.L.nice),
+                           lazy_l = to_vgpr(P.L.lazy), chain_max = to_vgpr(P.chain);
+            const unsigned pflags = to_vgpr((P.L.parser == P_SLOW ? 1u : 0u) | (P.strategy == 2 ? 2u : 0u) |
+                                            (P.strategy == 3 ? 4u : 0u) | (P.strategy == 1 ? 8u : 0u));
+            const bool lazy = (pflags & 1u) != 0, no_match = (pflags & 2u) != 0, rle = (pflags & 4u) != 0,
+                       filtered = (pflags & 8u) != 0;
             unsigned p = a, l0 = 0, d0 = 0;
             bool have0 = false;
             // Each iteration is one predicated step for every lane:
@@ -732,7 +746,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
                 const uint64_t cv = W.qw(cc + l), qv = W.qw(q + l);
                 const unsigned k = eq_bytes(cv, qv);
                 const bool ch = !st && !mt;
-                const bool term = ch && (c == NONE || q - c > P.max_dist || chain_left == 0);
+                const bool term = ch && (c == NONE || q - c > max_dist || chain_left == 0);
                 const bool test = ch && !term;
                 const bool quick = test && best < maxl && cb == qb && k > 0;
                 const bool go_match = quick && k == 8 && maxl > 8;
@@ -753,8 +767,8 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
                 if (st) {
                     maxl = wn - q < (unsigned)MAX_MATCH ? wn - q : (unsigned)MAX_MATCH;
                     c = rle ? (q > 0 ? q - 1 : NONE) : pn;
-                    chain_left = rle ? 1u : (thr >= P.L.good ? chain_max >> 2 : chain_max);
-                    nice = rle ? maxl : (P.L.nice < maxl ? P.L.nice : maxl);
+                    chain_left = rle ? 1u : (thr >= good ? chain_max >> 2 : chain_max);
+                    nice = rle ? maxl : (nice_l < maxl ? nice_l : maxl);
                 } else if (advance) {
                     c = pn;
                 }
@@ -763,7 +777,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
                 if (found) {
                     unsigned lr = best;
                     if (best > thr && best <= 5 &&
-                        (P.strategy == 1 || (best == (unsigned)MIN_MATCH && bd > (unsigned)TOO_FAR)))
+                        (filtered || (best == (unsigned)MIN_MATCH && bd > (unsigned)TOO_FAR)))
                         lr = thr;
                     // f_slow / f_fast decision
                     bool lit = false, emit = false;
@@ -786,7 +800,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
                         bm |= 1ull << (p - a);
                         ++p;
                     }
-                    if (!emit && have0 && p < b && !(lazy && l0 < P.L.lazy && p + 1 < wn)) {
+                    if (!emit && have0 && p < b && !(lazy && l0 < lazy_l && p + 1 < wn)) {
                         emit = true;
                         el = l0;
                         ed = d0;

@@ -74,7 +74,10 @@ constexpr uint32_t TOK_EXIT = 0x20000000u;  // the queue is empty: the lane is d
 #endif
 constexpr int KLIT = BPMD3_KLIT;   // symbols decoded per iteration when literals lead (bytes queue in one u32)
 constexpr int KCL = 4;    // code-length symbols per iteration (pass 1; 4 x 14 bits fit the reader)
-constexpr int KNIB = 16;  // code lengths placed per iteration (pass 2; a multiple of 8)
+#ifndef BPMD3_KNIB
+#define BPMD3_KNIB 16
+#endif
+constexpr int KNIB = BPMD3_KNIB;  // code lengths placed per iteration (pass 2; a multiple of 8, at most 32)
 
 enum : uint32_t { S_TYPE, S_DATA, S_SHDR, S_SCOPY, S_DYN, S_PASS1, S_BUILD, S_PASS2, S_DONE };
 
