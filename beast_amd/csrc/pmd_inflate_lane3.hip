@@ -106,17 +106,6 @@ template <int NB>
 __device__ __forceinline__ uint32_t canon_min(const uint32_t (&Q)[NB], uint32_t c)
 {
     const uint32_t k1 = (c + 1) << 15;
-#ifdef BPMD3_MIN3ASM
-    // v_min3 chain written out: the compiler otherwise splits part of it
-    // into two-operand mins
-    uint32_t d[NB];
-#pragma unroll
-    for (int i = 0; i < NB; ++i) d[i] = Q[i] - k1;
-    uint32_t m = d[0];
-#pragma unroll
-    for (int i = 1; i + 1 < NB; i += 2) asm("v_min3_u32 %0, %1, %2, %3" : "=v"(m) : "v"(m), "v"(d[i]), "v"(d[i + 1]));
-    if (NB % 2 == 0) m = __builtin_elementwise_min(m, d[NB - 1]);
-#else
     uint32_t m = Q[0] - k1;
 #pragma unroll
     for (int i = 1; i + 1 < NB; i += 2) {
@@ -124,7 +113,6 @@ __device__ __forceinline__ uint32_t canon_min(const uint32_t (&Q)[NB], uint32_t 
         m = __builtin_elementwise_min(m, __builtin_elementwise_min(x, y));
     }
     if (NB % 2 == 0) m = __builtin_elementwise_min(m, Q[NB - 1] - k1);
-#endif
     return m;
 }
 
@@ -314,29 +302,6 @@ __device__ __forceinline__ void expander(uint8_t* T, bool valid, uint32_t m, uin
                                          uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
                                          const uint32_t* __restrict__ hist_len, uint32_t hist_max, bool queue)
 {
-#ifdef BPMD3_EXP_MIN
-    // timing experiment: take tokens without expanding them (decoder alone)
-    {
-        bool ex = !queue && !valid;
-        uint32_t tl = 0;
-        for (;;) {
-            if (!__ballot(!ex)) break;
-            const uint32_t hd = lds_load(T + O_HEAD);
-            compiler_fence();
-            while (!ex && tl != hd) {
-                const uint2 e = *(const uint2*)(T + ring_at(tl));
-                ++tl;
-                if (e.y & TOK_END) { out_len[m] = e.x; status[m] = (int32_t)(int8_t)(e.y & 0xffu); ex = !queue; }
-                else if (e.y & TOK_NEW) m = e.x;
-                else if (e.y & TOK_EXIT) ex = true;
-            }
-            compiler_fence();
-            lds_store(T + O_TAIL, tl);
-            __builtin_amdgcn_s_sleep(BPMD3_ESLEEP);
-        }
-        return;
-    }
-#endif
     uint8_t* o = out;
     uint32_t cap = 0, hist = 0;
     auto slot = [&](uint32_t mm) {
@@ -442,10 +407,6 @@ __device__ __forceinline__ void expander(uint8_t* T, bool valid, uint32_t m, uin
                 cq += adv;
                 crem -= adv;
             }
-#ifdef BPMD3_EXP_NOMEM
-            ld = false;
-            cst = false;
-#endif
             if (ld) {
                 // 16 (32) bytes from src: the bytes used all lie in [src, cq);
                 // the rest may run into the next slot (never stored)
