@@ -437,11 +437,32 @@ __device__ void build_trees(HuffLds& H, Prof& pf)
     used_l = used_l < 2 ? 2 : used_l;
     used_d = used_d < 2 ? 2 : used_d;
     wave_sync();
-    // --- bitonic sort of 512 keys (4 compare-exchanges per lane per stage)
-    for (unsigned k = 2; k <= 512; k <<= 1) {
+    // --- compact the used keys to the front (lit keys stay below dist keys:
+    // bit 31) so the sort covers the next power of two >= their count, not 512
+    const unsigned used = (unsigned)__builtin_amdgcn_readfirstlane((int)(used_l + used_d));
+    const unsigned P = used <= 128 ? 128u : used <= 256 ? 256u : 512u;
+    {
+        uint32_t kv[5];
+#pragma unroll
+        for (unsigned t = 0; t < 5; ++t) kv[t] = H.keys[lane + t * WAVE];
+        wave_sync();
+        unsigned at = 0;
+#pragma unroll
+        for (unsigned t = 0; t < 5; ++t) {
+            const bool v = kv[t] != 0xFFFFFFFFu;
+            const uint64_t bm = ballot(v);
+            if (v) H.keys[at + popc_below(bm)] = kv[t];
+            at += (unsigned)__builtin_popcountll(bm);
+        }
+        for (unsigned i = at + lane; i < P; i += WAVE) H.keys[i] = 0xFFFFFFFFu;
+        wave_sync();
+    }
+    // --- bitonic sort of P keys (P / 128 compare-exchanges per lane per stage)
+    for (unsigned k = 2; k <= P; k <<= 1) {
         for (unsigned j = k >> 1; j > 0; j >>= 1) {
 #pragma unroll
             for (unsigned t = 0; t < 4; ++t) {
+                if (t >= P / 128) break;
                 const unsigned i = lane + t * WAVE;
                 const unsigned lo = ((i & ~(j - 1)) << 1) | (i & (j - 1)), hi = lo + j;
                 const uint32_t x = H.keys[lo], y = H.keys[hi];
