@@ -603,7 +603,7 @@ __device__ __forceinline__ void canonical_codes(HuffLds& H, unsigned base, unsig
         // next_code[b] = (next_code[b-1] + cnt[b-1]) << 1
         uint32_t code = 0;
         for (unsigned b = 1; b <= lz::MAX_BITS; ++b) {
-            const uint32_t cprev = __shfl(cnt, b - 1);
+            const uint32_t cprev = (uint32_t)__builtin_amdgcn_readlane((int)cnt, (int)(b - 1));
             code = (code + (b == 1 ? 0u : cprev)) << 1;
             if (lane == b) next = code;
         }
@@ -614,7 +614,7 @@ __device__ __forceinline__ void canonical_codes(HuffLds& H, unsigned base, unsig
         uint32_t code = 0;
         for (unsigned b = 1; b <= lz::MAX_BITS; ++b) {
             const uint64_t m = ballot(len == b);
-            const uint32_t nb = __shfl(next, b);
+            const uint32_t nb = (uint32_t)__builtin_amdgcn_readlane((int)next, (int)b);
             if (len == b) code = nb + popc_below(m);
             if (lane == b) next += (uint32_t)__builtin_popcountll(m);
         }
@@ -955,7 +955,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
                         atomicAdd(&H.bf[s], 1u);
                     });
                 }
-                run_carry += __shfl(incl, WAVE - 1);
+                run_carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
             }
             nrle = run_carry;
             wave_sync();
@@ -1035,7 +1035,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
         nbits += (H.codes[DIST_IDX + s] >> 16) + nx;
     });
     const uint32_t incl = wave_scan_incl(nbits);
-    const uint32_t tok_bits = __shfl(incl, WAVE - 1);
+    const uint32_t tok_bits = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     const uint32_t eob_len = H.codes[EOB] >> 16;
     const unsigned ob = (unsigned)((uintptr_t)(o.dst + o.opos) & 3);
     const uint32_t start_bits = ob * 8 + o.cbits;
@@ -1087,7 +1087,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
                 atomicOr(&ow[bp >> 5], v << sh);
                 if (sh + nb > 32) atomicOr(&ow[(bp >> 5) + 1], v >> (32 - sh));
             }
-            at += __shfl(incl2, WAVE - 1);
+            at += (uint32_t)__builtin_amdgcn_readlane((int)incl2, 63);
         }
     }
     pf.lap(13);

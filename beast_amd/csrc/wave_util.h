@@ -9,45 +9,53 @@ namespace bpmd {
 
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); asm volatile("" ::: "memory"); }
 
+// DPP steps (GFX9 encodings): row_shr:n shifts within rows of 16 lanes,
+// row_bcast:15 / row_bcast:31 carry a row's last lane into the next row(s);
+// lanes with nothing to read take 0 (the identity of + and unsigned max).
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ uint32_t dpp0(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, false);
+}
+
+// inclusive scans in 6 DPP steps (no LDS round trip, unlike shuffles)
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x)
+{
+    x += dpp0<0x111>(x);        // row_shr:1
+    x += dpp0<0x112>(x);        // row_shr:2
+    x += dpp0<0x114>(x);        // row_shr:4
+    x += dpp0<0x118>(x);        // row_shr:8
+    x += dpp0<0x142, 0xa>(x);   // row_bcast:15 -> rows 1, 3
+    x += dpp0<0x143, 0xc>(x);   // row_bcast:31 -> rows 2, 3
+    return x;
+}
+
+__device__ __forceinline__ uint32_t wave_scan_maxu(uint32_t x)
+{
+    x = max(x, dpp0<0x111>(x));
+    x = max(x, dpp0<0x112>(x));
+    x = max(x, dpp0<0x114>(x));
+    x = max(x, dpp0<0x118>(x));
+    x = max(x, dpp0<0x142, 0xa>(x));
+    x = max(x, dpp0<0x143, 0xc>(x));
+    return x;
+}
+
 __device__ __forceinline__ uint32_t wave_sum(uint32_t x)
 {
-#pragma unroll
-    for (unsigned d = 1; d < WAVE; d <<= 1) x += __shfl_xor(x, d);
-    return x;
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_incl(x), 63);
 }
 
 __device__ __forceinline__ uint32_t wave_maxu(uint32_t x)
 {
-#pragma unroll
-    for (unsigned d = 1; d < WAVE; d <<= 1) {
-        const uint32_t y = __shfl_xor(x, d);
-        x = x > y ? x : y;
-    }
-    return x;
-}
-
-__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x)
-{
-    const unsigned lane = lane_id();
-#pragma unroll
-    for (unsigned d = 1; d < WAVE; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d);
-        x += lane >= d ? y : 0u;   // select: a shuffle must not sink under divergence
-    }
-    return x;
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_maxu(x), 63);
 }
 
 // exclusive prefix max; lane 0 gets `ident`
 __device__ __forceinline__ uint32_t wave_scan_max_excl(uint32_t x, uint32_t ident)
 {
-    const unsigned lane = lane_id();
-#pragma unroll
-    for (unsigned d = 1; d < WAVE; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d);
-        x = (lane >= d && y > x) ? y : x;
-    }
-    const uint32_t e = __shfl_up(x, 1);
-    return lane == 0 ? ident : (e > ident ? e : ident);
+    const uint32_t e = __shfl_up(wave_scan_maxu(x), 1);
+    return lane_id() == 0 ? ident : (e > ident ? e : ident);
 }
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
