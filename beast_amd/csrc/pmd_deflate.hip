@@ -234,7 +234,11 @@ struct LaneToks {
 };
 
 // Calls f(is_match, lit_or_len, dist) for every owned token in order.
-template <class F>
+// SINGLE: one call site, for bodies that are cheap to run whole for either
+// kind (a wave then runs one body per token instead of both, which pays off
+// when matches are common); otherwise a literal and a match call site (the
+// wave skips the match body when no lane has a match: binary data).
+template <bool SINGLE = false, class F>
 __device__ __forceinline__ void for_tokens(const LaneToks& T, const uint16_t* tok, unsigned a0, F f)
 {
     if (T.rem_kind == 1) f(true, T.rem_len, T.rem_dist);
@@ -248,7 +252,11 @@ __device__ __forceinline__ void for_tokens(const LaneToks& T, const uint16_t* to
         m &= m - 1;
         const unsigned pos = T.a + t;
         const uint32_t e = tok[pos - a0];
-        if (e & 0x8000u) {
+        const bool mt = (e & 0x8000u) != 0;
+        if (SINGLE) {
+            const unsigned d = (mt && pos + 1 < T.b) ? (unsigned)tok[pos + 1 - a0] + 1 : T.lastdist;
+            f(mt, mt ? (e & 0xFFu) + 3 : e, d);
+        } else if (mt) {
             const unsigned d = pos + 1 < T.b ? (unsigned)tok[pos + 1 - a0] + 1 : T.lastdist;
             f(true, (e & 0xFFu) + 3, d);
         } else {
@@ -695,6 +703,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
     T.lastdist = 0;
     T.a = T.b = 0;
     uint32_t hdr_bits = 0, blcodes = 0, lcodes = 0, dcodes = 0, nrle = 0;
+    uint32_t n_tok = 0, n_match = 0;   // tokens and matches of the chunk (after the histogram pass: whole wave)
 
     if (!stored_only) {
         W.ws = load_window(S, msg + wb, wn);
@@ -891,13 +900,17 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
         }
         wave_sync();
         for_tokens(T, S.b.tok, a0, [&](bool is_match, unsigned v, unsigned dist) {
+            ++n_tok;
             if (!is_match) { atomicAdd(&H.lf[v], 1u); return; }
+            ++n_match;
             unsigned s, nx, xv;
             len_code(v, s, nx, xv);
             atomicAdd(&H.lf[s], 1u);
             dist_code(dist, s, nx, xv);
             atomicAdd(&H.df[s], 1u);
         });
+        n_tok = wave_sum(n_tok);
+        n_match = wave_sum(n_match);
         wave_sync();
         if (lane == 0) H.lf[EOB] = 1;
         wave_sync();
@@ -1026,14 +1039,19 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
     wave_sync();
     // per-lane token bits
     uint32_t nbits = 0;
-    for_tokens(T, S.b.tok, a0, [&](bool is_match, unsigned v, unsigned dist) {
-        if (!is_match) { nbits += H.codes[v] >> 16; return; }
+    // matches in at least a quarter of the tokens: one token body per step
+    const bool dense = (unsigned)__builtin_amdgcn_readfirstlane((int)n_match) * 4 > n_tok;
+    auto count_bits = [&](bool is_match, unsigned v, unsigned dist) {
         unsigned s, nx, xv;
-        len_code(v, s, nx, xv);
-        nbits += (H.codes[s] >> 16) + nx;
-        dist_code(dist, s, nx, xv);
-        nbits += (H.codes[DIST_IDX + s] >> 16) + nx;
-    });
+        len_code(is_match ? v : 3u, s, nx, xv);
+        nbits += (H.codes[is_match ? s : v] >> 16) + (is_match ? nx : 0u);
+        if (is_match) {
+            dist_code(dist, s, nx, xv);
+            nbits += (H.codes[DIST_IDX + s] >> 16) + nx;
+        }
+    };
+    if (dense) for_tokens<true>(T, S.b.tok, a0, count_bits);
+    else for_tokens<false>(T, S.b.tok, a0, count_bits);
     const uint32_t incl = wave_scan_incl(nbits);
     const uint32_t tok_bits = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     const uint32_t eob_len = H.codes[EOB] >> 16;
@@ -1094,21 +1112,22 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
     {
         BitOr bw;
         bw.start(ow, start_bits + hdr_bits + (incl - nbits));
-        for_tokens(T, S.b.tok, a0, [&](bool is_match, unsigned v, unsigned dist) {
-            if (!is_match) {
-                const uint32_t c = H.codes[v];
-                bw.put(c & 0xFFFFu, c >> 16);
-                return;
-            }
+        auto emit = [&](bool is_match, unsigned v, unsigned dist) {
+            // literal: its code; match: length code + extra, then distance
+            // code + extra (each <= 28 bits, one put each)
             unsigned s, nx, xv;
-            len_code(v, s, nx, xv);
-            uint32_t c = H.codes[s];
-            bw.put((c & 0xFFFFu) | (xv << (c >> 16)), (c >> 16) + nx);
-            dist_code(dist, s, nx, xv);
-            c = H.codes[DIST_IDX + s];
-            bw.put(c & 0xFFFFu, c >> 16);
-            if (nx) bw.put(xv, nx);
-        });
+            len_code(is_match ? v : 3u, s, nx, xv);
+            const uint32_t c = H.codes[is_match ? s : v];
+            const unsigned l1 = c >> 16;
+            bw.put((c & 0xFFFFu) | (is_match ? xv << l1 : 0u), l1 + (is_match ? nx : 0u));
+            if (is_match) {
+                dist_code(dist, s, nx, xv);
+                const uint32_t c2 = H.codes[DIST_IDX + s];
+                bw.put((c2 & 0xFFFFu) | (xv << (c2 >> 16)), (c2 >> 16) + nx);
+            }
+        };
+        if (dense) for_tokens<true>(T, S.b.tok, a0, emit);
+        else for_tokens<false>(T, S.b.tok, a0, emit);
         bw.flush();
     }
     wave_sync();
