@@ -50,12 +50,13 @@ LZ_HD Level level_params(int level)
 }
 
 // Chain limit the GPU encoder uses: the level table's, capped at
-// BPMD_CHAIN_CAP for messages of one 4 KiB chunk (C3 corpus at level 6: cap 4
-// costs +5.6 % size against Beast) and at
-// BPMD_CHAIN_CAP_MULTI (0 = the table's value) for longer messages: 16 keeps
-// configs[3] within the size tolerance (1.09x Beast) at 13.5 vs 8.6 GiB/s.
+// BPMD_CHAIN_CAP for messages of one 4 KiB chunk (C3 corpus at level 6, round
+// 2 build: cap 4 / 8 / 16 = 37.5 / 33.9 / 30.0 GiB/s at 1.056 / 1.038 / 1.020x
+// Beast's size) and at BPMD_CHAIN_CAP_MULTI (0 = the table's
+// value) for longer messages: 16 keeps configs[3] within the size tolerance
+// (1.09x Beast; 8 would give 1.11x).
 #ifndef BPMD_CHAIN_CAP
-#define BPMD_CHAIN_CAP 4
+#define BPMD_CHAIN_CAP 8
 #endif
 #ifndef BPMD_CHAIN_CAP_MULTI
 #define BPMD_CHAIN_CAP_MULTI 16
