@@ -275,28 +275,46 @@ __device__ __forceinline__ uint32_t pack_code(uint32_t code, unsigned len)
 // Two-queue merge for one tree, run by one lane (lit on lane 0, dist on lane
 // 1 at the same time).  Leaves are the sorted keys [kb, kb + m); internal
 // node k is node m + k; parent[] gets node ids relative to the tree base.
+// Branch-free: each queue's next TWO weights are held in registers, a pick
+// is a compare and selects, and the weight two places ahead in the queue it
+// took from is loaded for the pick after next (a lane-divergent branchy pick
+// spent most of its instructions on exec masks and waited on every load).
 __device__ __forceinline__ void merge_tree(HuffLds& H, unsigned kb, unsigned m, unsigned ib, unsigned pb)
 {
+    auto leaf = [&](unsigned i) -> uint32_t {   // weight of leaf i, 0 past the leaves
+        const uint32_t k = H.keys[kb + (i < m ? i : m - 1)];
+        return i < m ? (k >> 9) & 0x3FFFFFu : 0u;
+    };
     unsigned li = 0, ii = 0;
-    uint32_t kw = m ? (H.keys[kb] >> 9) & 0x3FFFFFu : 0;
+    uint32_t kw = leaf(0), kw1 = leaf(1);   // leaves li, li + 1
+    uint32_t iq = 0, iq1 = 0;               // internal ii, ii + 1 (valid below k)
     for (unsigned k = 0; k + 1 < m; ++k) {
-        uint32_t w0, w1;
-        unsigned id0, id1;
-        {
-            const uint32_t iwv = ii < k ? H.iw[ib + ii] : 0xFFFFFFFFu;
-            const bool leaf = li < m && (ii >= k || kw <= iwv);
-            if (leaf) { w0 = kw; id0 = li++; kw = li < m ? (H.keys[kb + li] >> 9) & 0x3FFFFFu : 0; }
-            else { w0 = iwv; id0 = m + ii++; }
+        uint32_t w[2];
+        unsigned id[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const bool have_i = ii < k;
+            const bool take_leaf = li < m && (!have_i || kw <= iq);
+            w[t] = take_leaf ? kw : iq;
+            id[t] = take_leaf ? li : m + ii;
+            // the queue that gave up its head: next weight moves up, the one
+            // after it is loaded (internal weights past k - 1 are patched below)
+            const uint32_t nl = leaf(li + 2);
+            const uint32_t ni = H.iw[ib + (ii + 2 < 320 - ib ? ii + 2 : ii)];
+            kw = take_leaf ? kw1 : kw;
+            kw1 = take_leaf ? nl : kw1;
+            iq = take_leaf ? iq : iq1;
+            iq1 = take_leaf ? iq1 : (uint32_t)ni;
+            li += take_leaf ? 1u : 0u;
+            ii += take_leaf ? 0u : 1u;
         }
-        {
-            const uint32_t iwv = ii < k ? H.iw[ib + ii] : 0xFFFFFFFFu;
-            const bool leaf = li < m && (ii >= k || kw <= iwv);
-            if (leaf) { w1 = kw; id1 = li++; kw = li < m ? (H.keys[kb + li] >> 9) & 0x3FFFFFu : 0; }
-            else { w1 = iwv; id1 = m + ii++; }
-        }
-        H.iw[ib + k] = (uint16_t)(w0 + w1);
-        H.parent[pb + id0] = (uint16_t)(m + k);
-        H.parent[pb + id1] = (uint16_t)(m + k);
+        const uint32_t ws = (uint16_t)(w[0] + w[1]);
+        H.iw[ib + k] = (uint16_t)ws;
+        H.parent[pb + id[0]] = (uint16_t)(m + k);
+        H.parent[pb + id[1]] = (uint16_t)(m + k);
+        // the new node is the queue's head or second when the queue had fewer
+        iq = ii == k ? ws : iq;
+        iq1 = ii + 1 == k ? ws : iq1;
     }
 }
 
