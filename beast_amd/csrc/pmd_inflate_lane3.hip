@@ -157,35 +157,26 @@ __device__ __forceinline__ uint32_t lowmask(uint32_t n) { return n >= 32 ? ~0u :
 template <int NB>
 __device__ __forceinline__ int make_canon(const uint32_t (&c)[16], uint32_t R, int type, Canon<NB>& t)
 {
-    uint32_t hi = 0, lo = 0;
-#pragma unroll
-    for (int l = NB; l >= 1; --l)
-        if (c[l]) lo = l;
-#pragma unroll
-    for (int l = 1; l <= NB; ++l)
-        if (c[l]) hi = l;
-    int left = 1;
-    bool over = false;
-#pragma unroll
-    for (int l = 1; l <= NB; ++l) {
-        left = 2 * left - (int)c[l];
-        over |= left < 0;
-    }
-    uint32_t lim = 0, cu = 0;
+    uint32_t lim = 0, cu = 0, nz = 0;   // nz: bit l set when some code has length l
 #pragma unroll
     for (int l = 1; l <= NB; ++l) {
         cu += c[l];
         lim += c[l] << (NB - l);
         t.Q[l - 1] = (lim << 15) | ((uint32_t)l << 11) | cu;
+        nz |= c[l] ? 1u << l : 0u;
     }
-    if (hi == 0) {   // empty code: a 1-bit root of invalid slots
+    if (nz == 0) {   // empty code: a 1-bit root of invalid slots
         t.root = 1;
         return 0;
     }
+    const uint32_t lo = (uint32_t)__builtin_ctz(nz), hi = 31u - (uint32_t)__builtin_clz(nz);
     const uint32_t r = R < hi ? R : hi;
     t.root = r < lo ? lo : r;
-    if (over) return ST_OVER_SUBSCRIBED_LENGTH;
-    if (left > 0 && (type == 0 || hi != 1)) return ST_INCOMPLETE_LENGTH_SET;
+    // The reference's running `left` (2^l minus the codes of length <= l)
+    // ends at 2^NB - lim; a prefix can only be over-subscribed if the whole
+    // Kraft sum is, since the partial sums only grow.
+    if (lim > (1u << NB)) return ST_OVER_SUBSCRIBED_LENGTH;
+    if (lim < (1u << NB) && (type == 0 || hi != 1)) return ST_INCOMPLETE_LENGTH_SET;
     return 0;
 }
 
