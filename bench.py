@@ -159,7 +159,11 @@ def _newest(pattern):
     import glob
     import re
     files = glob.glob(os.path.join(ROOT, "profiles", pattern))
-    key = lambda f: (int(re.search(r"r(\d+)", os.path.basename(f)).group(1)), os.path.getmtime(f))  # noqa: E731
+    # newest tag: round number, then the letter suffix (r02 < r02b < r02c);
+    # file times are no guide in a fresh checkout
+    def key(f):
+        t = re.match(r"r(\d+)([a-z]*)_", os.path.basename(f))
+        return (int(t.group(1)), t.group(2)) if t else (-1, "")
     return max(files, key=key) if files else None
 
 
