@@ -69,6 +69,15 @@ constexpr uint32_t TOK_EXIT = 0x20000000u;  // the queue is empty: the lane is d
 #ifndef BPMD3_ESLEEP
 #define BPMD3_ESLEEP 8
 #endif
+#ifndef BPMD3_DATA2
+#define BPMD3_DATA2 1
+#endif
+#ifndef BPMD3_XSTEPS
+#define BPMD3_XSTEPS 1   // extra data steps per iteration (DATA2)
+#endif
+#ifndef BPMD3_LITDW
+#define BPMD3_LITDW 1
+#endif
 #ifndef BPMD3_DPRIO
 #define BPMD3_DPRIO 3
 #endif
@@ -241,6 +250,7 @@ __device__ __forceinline__ uint4 finish_in(uint4 w, bool ld, uint32_t bi, uint32
 
 typedef uint4 uint4_u __attribute__((aligned(1)));
 typedef uint2 uint2_u __attribute__((aligned(1)));
+typedef uint32_t uint32_u __attribute__((aligned(1)));
 
 // Reads of the lane's own earlier output (match sources) are plain loads:
 // within one wave the vector L1 is coherent with the wave's own stores
@@ -355,9 +365,15 @@ __device__ __forceinline__ void expander(uint8_t* T, bool valid, uint32_t m, uin
             cst_pat = false;
         }
         if (bcnt) {
+            // one dword store (bytes past bcnt are overwritten by later
+            // output, as a chunk's spare tail), bytes only at the slot's end
+            if (BPMD3_LITDW && bdst + 4 <= cap) {
+                *(uint32_u*)(o + bdst) = bval;
+            } else {
 #pragma unroll
-            for (uint32_t j = 0; j < 4; ++j)
-                if (j < bcnt) o[bdst + j] = (uint8_t)(bval >> (8 * j));
+                for (uint32_t j = 0; j < 4; ++j)
+                    if (j < bcnt) o[bdst + j] = (uint8_t)(bval >> (8 * j));
+            }
             bcnt = 0;
         }
         if (crem) {
@@ -590,6 +606,147 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
         tc.root = 1;
         srem = 0;
     };
+    // nx <- the staged block sg (unmasked, tail applied), and the next block
+    // is staged (one 16-byte load)
+    auto pipe = [&]() {
+        // only a block that holds the payload's end needs finish_in's
+        // shift and tail work: a wave-uniform test keeps it off the rest
+        if (__ballot(sg_bi * 16 + 16 > s + n)) nx = finish_in(sg, sg_ld, sg_bi, s, n, tail, mk);
+        else nx = make_uint4(sg.x ^ mk, sg.y ^ mk, sg.z ^ mk, sg.w ^ mk);
+        const uint32_t b0 = blk * 16, E = (s + n + 3) & ~3u;
+        sg_ld = b0 < E;
+        if (sg_ld) sg = *(const uint4*)(A + b0 - 4 * in_shift(b0, E));
+        sg_bi = blk++;
+        nx_used = false;
+    };
+    // One token of a Huffman block: up to KLIT leading literals and a main
+    // symbol (see data_step's body).  Called once per iteration, and a second
+    // time for the lanes whose next input block is still unused (DATA2).
+    auto data_step = [&](uint32_t& enl, uint32_t& elit, uint32_t& emlen, uint32_t& edist) {
+        // Up to KLIT symbols per iteration: while there is room for them
+        // (input for KLIT - 1 literals plus a whole token, output for KLIT
+        // literals, so no event can occur among them) leading literals are
+        // taken directly; the first other symbol -- or, out of room, the
+        // first symbol of any kind -- is the iteration's main token, handled
+        // with the reference's checks below.  The KLIT code lengths come from
+        // registers, so their KLIT symbol lookups go out together.
+        refill();   // nb >= 33: with q.x, a 64-bit window
+        const uint64_t w = nb >= 64 ? bb : (bb | ((uint64_t)q.x << nb));
+        const bool multi = (tb + (int32_t)nb) >= 48 + 15 * (KLIT - 1) && pos + KLIT <= cap;
+        uint32_t kp[KLIT + 1], kc[KLIT], kL[KLIT], kx[KLIT];
+        bool kinv[KLIT];
+        kp[0] = 0;
+#pragma unroll
+        for (int k = 0; k < KLIT; ++k) {
+            kc[k] = rev15(w >> kp[k]);
+            const Sym y = canon_decode<15>(tl.Q, kc[k]);
+            kL[k] = y.L;
+            kx[k] = y.idx;
+            kinv[k] = y.inval;
+            kp[k + 1] = kp[k] + (y.inval ? 15u : y.L);
+        }
+        uint32_t kle[KLIT], ksb[KLIT];
+#pragma unroll
+        for (int k = 0; k < KLIT; ++k) {
+            kle[k] = LE[kL[k]];
+            ksb[k] = T[O_LIT + kx[k]];
+        }
+        uint32_t ks[KLIT];
+#pragma unroll
+        for (int k = 0; k < KLIT; ++k) ks[k] = ksb[k] + (kx[k] >= kle[k] ? 256u : 0u);
+        // leading literals taken directly
+        uint32_t nlit = 0, lbytes = 0;
+#pragma unroll
+        for (int k = 0; k < KLIT; ++k) {
+            const bool take = multi && nlit == (uint32_t)k && !kinv[k] && ks[k] < 256;
+            lbytes |= take ? ks[k] << (8 * k) : 0u;
+            nlit += take ? 1u : 0u;
+        }
+        uint32_t lit_bits = 0;
+#pragma unroll
+        for (int k = 1; k <= KLIT; ++k) lit_bits = nlit == (uint32_t)k ? kp[k] : lit_bits;
+        enl = nlit;
+        elit = lbytes;
+        pos += nlit;
+        // the main token: symbol nlit (none when all KLIT were literals)
+        uint32_t c15 = kc[0], L = kL[0], sym = ks[0];
+        bool kinv_m = kinv[0];
+#pragma unroll
+        for (int k = 1; k < KLIT; ++k) {
+            const bool here = nlit == (uint32_t)k;
+            c15 = here ? kc[k] : c15;
+            L = here ? kL[k] : L;
+            sym = here ? ks[k] : sym;
+            kinv_m = here ? kinv[k] : kinv_m;
+        }
+        const bool inval = kinv_m || sym >= 286;
+        drop_x(lit_bits);
+        // The main token, for the lanes that have one (nlit < KLIT), without
+        // divergent branches: every outcome is a select (a branch costs the
+        // wave its exec-mask instructions whether or not a lane takes it).
+        const bool mt = nlit < (uint32_t)KLIT;
+        refill();   // nb >= 33 again: the main token's <= 48 bits are in the window
+        const uint64_t w2 = nb >= 64 ? bb : (bb | ((uint64_t)q.x << nb));
+        const int32_t avail = tb + (int32_t)nb;
+        Sym y;
+        y.L = L;
+        y.idx = 0;
+        y.inval = inval;
+        // the fill rule only bites within 48 bits of the end of the input:
+        // a wave-uniform branch keeps its two canonical searches off the
+        // common path
+        const bool near_end = __ballot(mt && avail < 48) != 0;
+        uint32_t need_l = 0;
+        if (near_end && mt && avail < 48) need_l = canon_need<15>(tl, y, c15);
+        const bool is_len = !inval && sym > 256;
+        const uint32_t li = is_len ? sym - 257 : 0u;
+        const uint32_t xl = (li < 8 || li == 28) ? 0u : ((li - 4) >> 2);
+        uint32_t len = li < 8 ? li + 3 : (li == 28 ? 258u : (((4u + (li & 3)) << xl) + 3));
+        len += (uint32_t)(w2 >> L) & lowmask(xl);
+        const uint32_t used = L + (is_len ? xl : 0u);
+        const uint32_t d15 = rev15(w2 >> used);
+        const Sym yd = canon_decode<15>(td.Q, d15);
+        const uint32_t Ld = yd.L;
+        const uint32_t dsym = T[O_DST + yd.idx];
+        const bool invd = yd.inval || dsym >= 30;
+        const uint32_t xd = dsym < 4 ? 0u : (dsym >> 1) - 1;
+        uint32_t dist = dsym < 4 ? dsym + 1 : (((2u + (dsym & 1)) << xd) + 1);
+        dist += (uint32_t)(w2 >> (used + Ld)) & lowmask(xd);
+        uint32_t need_d = 0;
+        if (near_end && mt && avail < 48 && is_len) need_d = canon_need<15>(td, yd, d15);
+        // event, in the reference's order: 0 token, 1 eob, 2 starved, 3 error
+        const bool s_m1 = (int32_t)used > avail || (int32_t)(used + need_d) > avail;
+        const bool s_m2 = (int32_t)(used + Ld + xd) > avail;
+        const uint32_t ev = (int32_t)need_l > avail ? 2u
+                            : inval               ? 3u
+                            : sym == 256          ? 1u
+                            : !is_len             ? 0u
+                            : s_m1                ? 2u
+                            : invd                ? 3u
+                            : s_m2                ? 2u
+                                                  : 0u;
+        const int32_t err = inval ? ST_INVALID_LITERAL_LENGTH : ST_INVALID_DISTANCE_CODE;
+        const bool is_match = ev == 0 && is_len;
+        drop_x(mt && ev < 2 ? (is_match ? used + Ld + xd : used) : 0u);
+        // output checks in the reference's order (inflate_stream.ipp:475-514)
+        const bool tok = mt && ev == 0;
+        const bool c_raw = raw && pos >= cap;
+        const bool c_dist = is_match && dist > pos + hist;
+        const bool c_full = pos >= cap;
+        uint32_t olen = is_match ? len : 1u;
+        const bool c_trunc = pos + olen > cap;
+        olen = c_trunc ? cap - pos : olen;
+        const bool emit = tok && !c_raw && !c_dist && !c_full;
+        const bool stop_full = tok && (c_raw || (!c_dist && (c_full || c_trunc)));
+        const bool stop_dist = tok && !c_raw && c_dist;
+        result = stop_full ? full_status : stop_dist ? ST_INVALID_DISTANCE : (mt && ev == 3) ? err : result;
+        st = (stop_full || stop_dist || (mt && ev >= 2)) ? (uint32_t)S_DONE : (mt && ev == 1) ? (uint32_t)S_TYPE : st;
+        emlen = emit && is_match ? olen : 0u;
+        edist = emit && is_match ? dist : 0u;
+        enl = emit && !is_match ? 1u : enl;
+        elit = emit && !is_match ? sym : elit;
+        pos += emit ? olen : 0u;
+    };
     if (valid) begin(m);
     L3_DECL;
     L3_LAPDECL;
@@ -628,17 +785,8 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
         if (__ballot(st != S_DATA && st != S_DONE && st != S_SCOPY && st != S_TYPE)) L3_CNT(3);
 #endif
         // ---- the input pipeline (the only global memory the decoder touches)
-        if (nx_used) {
-            // only a block that holds the payload's end needs finish_in's
-            // shift and tail work: a wave-uniform test keeps it off the rest
-            if (__ballot(sg_bi * 16 + 16 > s + n)) nx = finish_in(sg, sg_ld, sg_bi, s, n, tail, mk);
-            else nx = make_uint4(sg.x ^ mk, sg.y ^ mk, sg.z ^ mk, sg.w ^ mk);
-            const uint32_t b0 = blk * 16, E = (s + n + 3) & ~3u;
-            sg_ld = b0 < E;
-            if (sg_ld) sg = *(const uint4*)(A + b0 - 4 * in_shift(b0, E));
-            sg_bi = blk++;
-            nx_used = false;
-        }
+        const bool piped = nx_used;   // sg is re-issued now: not ready for DATA2
+        if (nx_used) pipe();
         const uint32_t taken = lds_load(T + O_TAIL);
         compiler_fence();
         const bool room = head - taken < RING;
@@ -656,131 +804,7 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
         const uint32_t st0 = st;
         const uint32_t head0 = head;
         L3_LAP(0);
-        if (st == S_DATA && room) {
-            // Up to KLIT symbols per iteration: while there is room for them
-            // (input for KLIT - 1 literals plus a whole token, output for KLIT
-            // literals, so no event can occur among them) leading literals are
-            // taken directly; the first other symbol -- or, out of room, the
-            // first symbol of any kind -- is the iteration's main token, handled
-            // with the reference's checks below.  The KLIT code lengths come from
-            // registers, so their KLIT symbol lookups go out together.
-            refill();   // nb >= 33: with q.x, a 64-bit window
-            const uint64_t w = nb >= 64 ? bb : (bb | ((uint64_t)q.x << nb));
-            const bool multi = (tb + (int32_t)nb) >= 48 + 15 * (KLIT - 1) && pos + KLIT <= cap;
-            uint32_t kp[KLIT + 1], kc[KLIT], kL[KLIT], kx[KLIT];
-            bool kinv[KLIT];
-            kp[0] = 0;
-#pragma unroll
-            for (int k = 0; k < KLIT; ++k) {
-                kc[k] = rev15(w >> kp[k]);
-                const Sym y = canon_decode<15>(tl.Q, kc[k]);
-                kL[k] = y.L;
-                kx[k] = y.idx;
-                kinv[k] = y.inval;
-                kp[k + 1] = kp[k] + (y.inval ? 15u : y.L);
-            }
-            uint32_t kle[KLIT], ksb[KLIT];
-#pragma unroll
-            for (int k = 0; k < KLIT; ++k) {
-                kle[k] = LE[kL[k]];
-                ksb[k] = T[O_LIT + kx[k]];
-            }
-            uint32_t ks[KLIT];
-#pragma unroll
-            for (int k = 0; k < KLIT; ++k) ks[k] = ksb[k] + (kx[k] >= kle[k] ? 256u : 0u);
-            // leading literals taken directly
-            uint32_t nlit = 0, lbytes = 0;
-#pragma unroll
-            for (int k = 0; k < KLIT; ++k) {
-                const bool take = multi && nlit == (uint32_t)k && !kinv[k] && ks[k] < 256;
-                lbytes |= take ? ks[k] << (8 * k) : 0u;
-                nlit += take ? 1u : 0u;
-            }
-            uint32_t lit_bits = 0;
-#pragma unroll
-            for (int k = 1; k <= KLIT; ++k) lit_bits = nlit == (uint32_t)k ? kp[k] : lit_bits;
-            enl = nlit;
-            elit = lbytes;
-            pos += nlit;
-            // the main token: symbol nlit (none when all KLIT were literals)
-            uint32_t c15 = kc[0], L = kL[0], sym = ks[0];
-            bool kinv_m = kinv[0];
-#pragma unroll
-            for (int k = 1; k < KLIT; ++k) {
-                const bool here = nlit == (uint32_t)k;
-                c15 = here ? kc[k] : c15;
-                L = here ? kL[k] : L;
-                sym = here ? ks[k] : sym;
-                kinv_m = here ? kinv[k] : kinv_m;
-            }
-            const bool inval = kinv_m || sym >= 286;
-            drop_x(lit_bits);
-            // The main token, for the lanes that have one (nlit < KLIT), without
-            // divergent branches: every outcome is a select (a branch costs the
-            // wave its exec-mask instructions whether or not a lane takes it).
-            const bool mt = nlit < (uint32_t)KLIT;
-            refill();   // nb >= 33 again: the main token's <= 48 bits are in the window
-            const uint64_t w2 = nb >= 64 ? bb : (bb | ((uint64_t)q.x << nb));
-            const int32_t avail = tb + (int32_t)nb;
-            Sym y;
-            y.L = L;
-            y.idx = 0;
-            y.inval = inval;
-            // the fill rule only bites within 48 bits of the end of the input:
-            // a wave-uniform branch keeps its two canonical searches off the
-            // common path
-            const bool near_end = __ballot(mt && avail < 48) != 0;
-            uint32_t need_l = 0;
-            if (near_end && mt && avail < 48) need_l = canon_need<15>(tl, y, c15);
-            const bool is_len = !inval && sym > 256;
-            const uint32_t li = is_len ? sym - 257 : 0u;
-            const uint32_t xl = (li < 8 || li == 28) ? 0u : ((li - 4) >> 2);
-            uint32_t len = li < 8 ? li + 3 : (li == 28 ? 258u : (((4u + (li & 3)) << xl) + 3));
-            len += (uint32_t)(w2 >> L) & lowmask(xl);
-            const uint32_t used = L + (is_len ? xl : 0u);
-            const uint32_t d15 = rev15(w2 >> used);
-            const Sym yd = canon_decode<15>(td.Q, d15);
-            const uint32_t Ld = yd.L;
-            const uint32_t dsym = T[O_DST + yd.idx];
-            const bool invd = yd.inval || dsym >= 30;
-            const uint32_t xd = dsym < 4 ? 0u : (dsym >> 1) - 1;
-            uint32_t dist = dsym < 4 ? dsym + 1 : (((2u + (dsym & 1)) << xd) + 1);
-            dist += (uint32_t)(w2 >> (used + Ld)) & lowmask(xd);
-            uint32_t need_d = 0;
-            if (near_end && mt && avail < 48 && is_len) need_d = canon_need<15>(td, yd, d15);
-            // event, in the reference's order: 0 token, 1 eob, 2 starved, 3 error
-            const bool s_m1 = (int32_t)used > avail || (int32_t)(used + need_d) > avail;
-            const bool s_m2 = (int32_t)(used + Ld + xd) > avail;
-            const uint32_t ev = (int32_t)need_l > avail ? 2u
-                                : inval               ? 3u
-                                : sym == 256          ? 1u
-                                : !is_len             ? 0u
-                                : s_m1                ? 2u
-                                : invd                ? 3u
-                                : s_m2                ? 2u
-                                                      : 0u;
-            const int32_t err = inval ? ST_INVALID_LITERAL_LENGTH : ST_INVALID_DISTANCE_CODE;
-            const bool is_match = ev == 0 && is_len;
-            drop_x(mt && ev < 2 ? (is_match ? used + Ld + xd : used) : 0u);
-            // output checks in the reference's order (inflate_stream.ipp:475-514)
-            const bool tok = mt && ev == 0;
-            const bool c_raw = raw && pos >= cap;
-            const bool c_dist = is_match && dist > pos + hist;
-            const bool c_full = pos >= cap;
-            uint32_t olen = is_match ? len : 1u;
-            const bool c_trunc = pos + olen > cap;
-            olen = c_trunc ? cap - pos : olen;
-            const bool emit = tok && !c_raw && !c_dist && !c_full;
-            const bool stop_full = tok && (c_raw || (!c_dist && (c_full || c_trunc)));
-            const bool stop_dist = tok && !c_raw && c_dist;
-            result = stop_full ? full_status : stop_dist ? ST_INVALID_DISTANCE : (mt && ev == 3) ? err : result;
-            st = (stop_full || stop_dist || (mt && ev >= 2)) ? (uint32_t)S_DONE : (mt && ev == 1) ? (uint32_t)S_TYPE : st;
-            emlen = emit && is_match ? olen : 0u;
-            edist = emit && is_match ? dist : 0u;
-            enl = emit && !is_match ? 1u : enl;
-            elit = emit && !is_match ? sym : elit;
-            pos += emit ? olen : 0u;
-        }
+        if (st == S_DATA && room) data_step(enl, elit, emlen, edist);
 
 
         L3_LAP(1);
@@ -1153,6 +1177,32 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
                 send_exit = false;
             }
         }
+#if BPMD3_DATA2
+        // ---- a second token for the lanes still in the same Huffman block
+        // with room in the ring and their next input block unused (so this
+        // step's refills cannot reach a block that is not loaded yet): the
+        // loop's fixed work -- input pipeline, ring tail, header test,
+        // publish and the wave's exit tests -- is then paid once per two
+        // tokens.  (~82 % of C2 data lanes qualify: a step reads 22 bits on
+        // average, a block holds 128.)
+#pragma unroll
+        for (int xs = 0; xs < BPMD3_XSTEPS; ++xs) {
+#if BPMD3_DATA2 >= 2
+            // (lanes that used their next block in the first step refill it
+            // now when its successor was staged in an earlier iteration)
+            if (xs == 0 && st0 == S_DATA && st == S_DATA && nx_used && !piped) pipe();
+#endif
+            if (!__ballot(st0 == S_DATA && st == S_DATA && !nx_used && head - taken < RING)) break;
+            uint32_t enl2 = 0, elit2 = 0, emlen2 = 0, edist2 = 0;
+            if (st0 == S_DATA && st == S_DATA && !nx_used && head - taken < RING)
+                data_step(enl2, elit2, emlen2, edist2);
+            const bool adv2 = enl2 != 0 || emlen2 != 0;
+            if (adv2) *(uint2*)(T + ring_at(head)) = make_uint2(elit2, enl2 | (emlen2 << 3) | (edist2 << 12));
+            compiler_fence();
+            head += adv2 ? 1u : 0u;
+            lds_store(T + O_HEAD, head);
+        }
+#endif
         // blocked on a full ring in every lane: leave the SIMD to the expander
         if (!__ballot(head != head0 || st != st0 || (st != S_DATA && st != S_SCOPY && st != S_DONE))) {
             L3_CNT(2);
