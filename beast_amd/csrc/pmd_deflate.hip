@@ -1211,7 +1211,10 @@ deflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
 // serial walk over the chunks would produce; only a stored block's padding to a byte
 // boundary depends on its start, and the stitch writes it there.
 constexpr unsigned SLOT = 4736;   // >= bpmd_deflate_upper_bound(CHUNK) + 2, 16-byte multiple
-constexpr int CHUNK_HIST = 4096;   // history bytes before each chunk (and before a takeover message)
+#ifndef BPMD_CHUNK_HIST
+#define BPMD_CHUNK_HIST 4096
+#endif
+constexpr int CHUNK_HIST = BPMD_CHUNK_HIST;   // history bytes before each chunk (and before a takeover message)
 
 __device__ __forceinline__ uint32_t chunk_count(uint32_t len, bool all)
 {
