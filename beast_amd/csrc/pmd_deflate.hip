@@ -82,7 +82,7 @@ struct alignas(16) DefLds {
     static constexpr unsigned W = HIST + CHUNK;
     // window bytes at byte offset `ws`; output bit buffer after the parse.  The
     // window has no slack (ws = 0): single-chunk 20480 B per wave, 8 waves per
-    // CU, history kernel 32768 B, 5 waves per CU; reads past the data land in `a` and are clamped by the lookahead, and
+    // CU, history kernel (2048 B of history) 26624 B, 6 waves per CU; reads past the data land in `a` and are clamped by the lookahead, and
     // the bit buffer's last words spill into lf[] only after lf is dead.
     uint32_t win[W / 4];
     union {
@@ -96,7 +96,7 @@ struct alignas(16) DefLds {
 };
 
 static_assert(sizeof(DefLds<0>) == 160 * 1024 / 8, "single-chunk deflate LDS: 8 waves per CU");
-static_assert(sizeof(DefLds<4096>) == 32768, "history deflate LDS: 5 waves per CU");
+static_assert(sizeof(DefLds<2048>) == 26624, "history deflate LDS: 6 waves per CU");
 static_assert(offsetof(HuffLds, lf) == 0, "bit buffer spill lands in lf[] (dead while packing)");
 
 struct Params {
@@ -1202,7 +1202,7 @@ deflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
 // ------------------------------------------------ chunk-parallel large messages
 // A message longer than one chunk (or any message of a context-takeover
 // batch) is encoded chunk by chunk IN PARALLEL: every 4 KiB chunk, with the
-// 4 KiB of input before it as history, becomes one block of its own in a
+// BPMD_CHUNK_HIST (2 KiB) of input before it as history, becomes one block of its own in a
 // scratch slot, starting at bit 0 (deflate_chunks_kernel); then one wave per
 // message stitches the blocks together at their bit offsets, applies the
 // client mask and appends Flush::sync's empty stored block header
@@ -1211,10 +1211,7 @@ deflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
 // serial walk over the chunks would produce; only a stored block's padding to a byte
 // boundary depends on its start, and the stitch writes it there.
 constexpr unsigned SLOT = 4736;   // >= bpmd_deflate_upper_bound(CHUNK) + 2, 16-byte multiple
-#ifndef BPMD_CHUNK_HIST
-#define BPMD_CHUNK_HIST 4096
-#endif
-constexpr int CHUNK_HIST = BPMD_CHUNK_HIST;   // history bytes before each chunk (and before a takeover message)
+constexpr int CHUNK_HIST = BPMD_CHUNK_HIST;   // (lz_core.h) history bytes before each chunk (and before a takeover message)
 
 __device__ __forceinline__ uint32_t chunk_count(uint32_t len, bool all)
 {
@@ -1260,7 +1257,7 @@ deflate_chunks_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict
     __shared__ DefLds<HIST> S;
     Prof pf;
     const uint32_t total = *n_items;
-    // chunks from a counter: 5 waves per CU leave one SIMD with two, whose
+    // chunks from a counter: 6 waves per CU leave two SIMDs with two, whose
     // waves would set the end of a static stride
     auto next = [&]() -> uint32_t {
         uint32_t v = 0;

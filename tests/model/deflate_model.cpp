@@ -305,3 +305,6 @@ extern "C" int dmodel_rle_check(const uint8_t* lens, int n, uint32_t* serial, ui
         if (serial[i] != runs[i]) return 0;
     return 1;
 }
+
+// history bytes before each chunk of a long message (the kernel's value)
+extern "C" int dmodel_chunk_hist() { return BPMD_CHUNK_HIST; }
