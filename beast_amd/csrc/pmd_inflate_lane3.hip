@@ -82,9 +82,12 @@ constexpr uint32_t TOK_EXIT = 0x20000000u;  // the queue is empty: the lane is d
 #define BPMD3_DPRIO 3
 #endif
 constexpr int KLIT = BPMD3_KLIT;   // symbols decoded per iteration when literals lead (bytes queue in one u32)
-constexpr int KCL = 4;    // code-length symbols per iteration (pass 1; 4 x 14 bits fit the reader)
+#ifndef BPMD3_KCL
+#define BPMD3_KCL 6
+#endif
+constexpr int KCL = BPMD3_KCL;   // code-length symbols per iteration (pass 1; a refill before each, <= 4 input dwords per iteration)
 #ifndef BPMD3_KNIB
-#define BPMD3_KNIB 16
+#define BPMD3_KNIB 32
 #endif
 constexpr int KNIB = BPMD3_KNIB;  // code lengths placed per iteration (pass 2; a multiple of 8, at most 32)
 
