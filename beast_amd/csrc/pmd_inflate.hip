@@ -54,7 +54,13 @@ namespace bpmd {
 constexpr unsigned RING = BPMD_RING;     // output history ring (bytes)
 constexpr unsigned RING_MASK = RING - 1;
 constexpr unsigned R_MAX = RING - 256;   // output bytes per round, at most
-constexpr unsigned IN_CAP = 2560;        // input window bytes
+#ifndef BPMD_IN_CAP
+#define BPMD_IN_CAP 2560
+#endif
+// input window bytes (a round's segments need (64 * 300 + 160) / 8 + 16 =
+// 2436).  2496 would bring WaveLds to 16 368 B, 10 waves per CU instead of 9,
+// but measured C5 inflate 33.9 -> 23.5 GiB/s: do not trim it.
+constexpr unsigned IN_CAP = BPMD_IN_CAP;
 constexpr unsigned IN_PAD = 32;
 constexpr unsigned WIN_WORDS = (IN_CAP + IN_PAD) / 4;
 constexpr unsigned TOT = BPMD_TOT;       // tokens per round, at most
@@ -81,6 +87,7 @@ struct alignas(16) WaveLds {
     } u;
     uint16_t tab[kEnough];
 };
+static_assert((WAVE * SEG_MAX_BITS + 160) / 8 + 16 <= IN_CAP, "a round's segments fit the input window");
 
 __device__ uint16_t g_fixed_lens[512];
 __device__ uint16_t g_fixed_dists[32];

@@ -69,15 +69,6 @@ constexpr uint32_t TOK_EXIT = 0x20000000u;  // the queue is empty: the lane is d
 #ifndef BPMD3_ESLEEP
 #define BPMD3_ESLEEP 8
 #endif
-#ifndef BPMD3_DATA2
-#define BPMD3_DATA2 1
-#endif
-#ifndef BPMD3_XSTEPS
-#define BPMD3_XSTEPS 1   // extra data steps per iteration (DATA2)
-#endif
-#ifndef BPMD3_LITDW
-#define BPMD3_LITDW 1
-#endif
 #ifndef BPMD3_DPRIO
 #define BPMD3_DPRIO 3
 #endif
@@ -370,7 +361,7 @@ __device__ __forceinline__ void expander(uint8_t* T, bool valid, uint32_t m, uin
         if (bcnt) {
             // one dword store (bytes past bcnt are overwritten by later
             // output, as a chunk's spare tail), bytes only at the slot's end
-            if (BPMD3_LITDW && bdst + 4 <= cap) {
+            if (bdst + 4 <= cap) {
                 *(uint32_u*)(o + bdst) = bval;
             } else {
 #pragma unroll
@@ -624,7 +615,7 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
     };
     // One token of a Huffman block: up to KLIT leading literals and a main
     // symbol (see data_step's body).  Called once per iteration, and a second
-    // time for the lanes whose next input block is still unused (DATA2).
+    // time for the lanes whose next input block is still unused.
     auto data_step = [&](uint32_t& enl, uint32_t& elit, uint32_t& emlen, uint32_t& edist) {
         // Up to KLIT symbols per iteration: while there is room for them
         // (input for KLIT - 1 literals plus a whole token, output for KLIT
@@ -788,7 +779,6 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
         if (__ballot(st != S_DATA && st != S_DONE && st != S_SCOPY && st != S_TYPE)) L3_CNT(3);
 #endif
         // ---- the input pipeline (the only global memory the decoder touches)
-        const bool piped = nx_used;   // sg is re-issued now: not ready for DATA2
         if (nx_used) pipe();
         const uint32_t taken = lds_load(T + O_TAIL);
         compiler_fence();
@@ -1180,22 +1170,14 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
                 send_exit = false;
             }
         }
-#if BPMD3_DATA2
         // ---- a second token for the lanes still in the same Huffman block
         // with room in the ring and their next input block unused (so this
         // step's refills cannot reach a block that is not loaded yet): the
         // loop's fixed work -- input pipeline, ring tail, header test,
         // publish and the wave's exit tests -- is then paid once per two
-        // tokens.  (~82 % of C2 data lanes qualify: a step reads 22 bits on
-        // average, a block holds 128.)
-#pragma unroll
-        for (int xs = 0; xs < BPMD3_XSTEPS; ++xs) {
-#if BPMD3_DATA2 >= 2
-            // (lanes that used their next block in the first step refill it
-            // now when its successor was staged in an earlier iteration)
-            if (xs == 0 && st0 == S_DATA && st == S_DATA && nx_used && !piped) pipe();
-#endif
-            if (!__ballot(st0 == S_DATA && st == S_DATA && !nx_used && head - taken < RING)) break;
+        // tokens (about half of the data lanes take it; a
+        // third step, or refilling the input block first, measured neutral).
+        if (__ballot(st0 == S_DATA && st == S_DATA && !nx_used && head - taken < RING)) {
             uint32_t enl2 = 0, elit2 = 0, emlen2 = 0, edist2 = 0;
             if (st0 == S_DATA && st == S_DATA && !nx_used && head - taken < RING)
                 data_step(enl2, elit2, emlen2, edist2);
@@ -1205,7 +1187,6 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
             head += adv2 ? 1u : 0u;
             lds_store(T + O_HEAD, head);
         }
-#endif
         // blocked on a full ring in every lane: leave the SIMD to the expander
         if (!__ballot(head != head0 || st != st0 || (st != S_DATA && st != S_SCOPY && st != S_DONE))) {
             L3_CNT(2);
