@@ -745,7 +745,7 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
     L3_DECL;
     L3_LAPDECL;
 #ifdef BPMD_PROF
-    unsigned long long l3x_[4] = {0, 0, 0, 0};
+    unsigned long long l3x_[4] = {0, 0, 0, 0}, l3dyn_ = 0;
 #endif
 
     for (;;) {
@@ -791,6 +791,7 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
         l3x_[1] += __builtin_popcountll(__ballot(st == S_DATA && room));
         l3x_[2] += __builtin_popcountll(__ballot(fin && !send_new));
         l3x_[3] += __builtin_popcountll(__ballot(st != S_DATA && st != S_DONE));
+        l3dyn_ += __builtin_popcountll(__ballot(st == S_DYN && !ring_empty));   // [7]
 #endif
         // this iteration's token
         uint32_t enl = 0, elit = 0, emlen = 0, edist = 0;
@@ -1197,7 +1198,10 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
     L3_LAPFLUSH();
 #ifdef BPMD_PROF
     if ((threadIdx.x & 63) == 0)
+    {
         for (int i = 0; i < 4; ++i) atomicAdd(&g_l3prof[12 + i], l3x_[i]);
+        atomicAdd(&g_l3prof[7], l3dyn_);
+    }
 #endif
 }
 

@@ -34,7 +34,7 @@ def main():
     L.bpmd_diag_lane3_counters(c, 1)
     ok = torch.equal(r.out.data[: n * size].view(n, size), torch.from_numpy(raw.reshape(n, size)).to(dev))
     w = n // 64
-    names = ["dec cycles", "dec iters", "dec sleeps", "dec hdr iters", "exp cycles", "exp iters", "exp sleeps", "-",
+    names = ["dec cycles", "dec iters", "dec sleeps", "dec hdr iters", "exp cycles", "exp iters", "exp sleeps", "lanes: header, ring not empty",
              "dec lap: input+tail", "dec lap: S_DATA", "dec lap: headers", "dec lap: publish+loop",
              "lanes: data, ring full", "lanes: data, room", "lanes: finished", "lanes: in headers"]
     for i, nm in enumerate(names):
