@@ -295,6 +295,37 @@ extern "C" int bpmd_mask_batch(uint8_t* d_data, const uint64_t* d_off, const uin
                                                                                                  : BPMD_R_OK;
 }
 
+extern "C" int bpmd_internal_frame(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint8_t* op,
+                                   const uint8_t* flags, const uint32_t* keys, const uint32_t* key_base,
+                                   uint32_t frame_max, uint32_t n, uint8_t* wire, const uint64_t* wire_off,
+                                   hipStream_t stream);
+
+// frame.hpp:134-175 header sizes over the write.hpp:463-545 frame loop
+extern "C" uint64_t bpmd_frame_wire_size(uint64_t payload_len, uint32_t frame_max, int masked)
+{
+    if (frame_max == 0) return 0;
+    const uint64_t frames = payload_len == 0 ? 1 : (payload_len + frame_max - 1) / frame_max;
+    const uint64_t last = payload_len - (frames - 1) * frame_max;
+    auto hdr = [&](uint64_t len) -> uint64_t { return (len <= 125 ? 2u : len <= 65535 ? 4u : 10u) + (masked ? 4u : 0u); };
+    return payload_len + (frames - 1) * hdr(frame_max) + hdr(last);
+}
+
+extern "C" int bpmd_frame_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint32_t* d_in_len,
+                                const uint8_t* d_op, const uint8_t* d_flags, const uint32_t* d_keys,
+                                const uint32_t* d_key_base, uint32_t frame_max, uint32_t n_msgs, uint8_t* d_wire,
+                                const uint64_t* d_wire_off, void* stream)
+{
+    if (n_msgs == 0) return BPMD_R_OK;
+    if (!d_in || !d_in_off || !d_in_len || !d_wire || !d_wire_off || frame_max == 0 || (d_keys && !d_key_base))
+        return BPMD_R_INVALID_ARGUMENT;
+    int r = bpmd_init();
+    if (r) return r;
+    return bpmd_internal_frame(d_in, d_in_off, d_in_len, d_op, d_flags, d_keys, d_key_base, frame_max, n_msgs, d_wire,
+                               d_wire_off, (hipStream_t)stream)
+               ? BPMD_R_HIP_ERROR
+               : BPMD_R_OK;
+}
+
 extern "C" int bpmd_utf8_check_batch(const uint8_t* d_data, const uint64_t* d_off, const uint32_t* d_len,
                                      uint32_t n_msgs, int32_t* d_result, void* stream)
 {

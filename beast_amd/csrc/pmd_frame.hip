@@ -213,6 +213,85 @@ slide_kernel(uint8_t* __restrict__ buf, const uint64_t* __restrict__ base, const
     }
 }
 
+
+// ---------------------------------------------------------------- frames
+// Send side of a message (write.hpp:463-545): the payload goes out in frames
+// of at most frame_max bytes, each with its header (frame.hpp:134-175): FIN
+// on the last, RSV1 and the opcode on the first (cont = 0 after), MASK and
+// the frame's own key (little-endian on the wire) for a client, whose frame
+// payload is then masked from the key's first byte.  One wave per message:
+// lanes 0..13 write the header bytes, then 16 payload bytes per lane per step
+// (a frame's 16-byte units start at frame offsets that are multiples of 4,
+// so every dword of a unit takes the key as it is).
+__device__ __forceinline__ uint32_t hdr_len(uint64_t len, bool masked)
+{
+    return (len <= 125 ? 2u : len <= 65535 ? 4u : 10u) + (masked ? 4u : 0u);
+}
+
+typedef uint4 uint4_fu __attribute__((aligned(1)));
+
+__global__ void __launch_bounds__(WAVE * WPB)
+frame_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint32_t* __restrict__ in_len,
+             const uint8_t* __restrict__ op, const uint8_t* __restrict__ flags, const uint32_t* __restrict__ keys,
+             const uint32_t* __restrict__ key_base, uint32_t frame_max, uint32_t n, uint8_t* __restrict__ wire,
+             const uint64_t* __restrict__ wire_off)
+{
+    const unsigned lane = threadIdx.x & (WAVE - 1);
+    for (uint32_t m = blockIdx.x * WPB + (threadIdx.x / WAVE); m < n; m += gridDim.x * WPB) {
+        const uint32_t nb = in_len[m];
+        const uint8_t* p = in + in_off[m];
+        uint8_t* w = wire + wire_off[m];
+        const uint32_t frames = nb == 0 ? 1u : (nb + frame_max - 1) / frame_max;
+        const bool masked = keys != nullptr;
+        const uint32_t kb = masked ? key_base[m] : 0u;
+        const uint32_t opc = op ? op[m] & 15u : 2u;
+        const bool rsv1 = flags ? (flags[m] & 1u) != 0 : true;
+        uint64_t wp = 0;
+        for (uint32_t f = 0; f < frames; ++f) {
+            const uint32_t a = f * frame_max, len = f + 1 < frames ? frame_max : nb - a;
+            const uint32_t key = masked ? keys[kb + f] : 0u;
+            // header bytes 0-7 in h0, 8-13 in h1 (frame.hpp:134-175)
+            const uint32_t b0 = (f + 1 == frames ? 0x80u : 0u) | (f == 0 && rsv1 ? 0x40u : 0u) | (f == 0 ? opc : 0u);
+            uint64_t h0, h1 = 0;
+            uint32_t hl;
+            if (len <= 125) {
+                h0 = b0 | (uint64_t)((masked ? 0x80u : 0u) | len) << 8;
+                hl = 2;
+            } else if (len <= 65535) {
+                h0 = b0 | (uint64_t)((masked ? 0x80u : 0u) | 126u) << 8 | (uint64_t)(len >> 8) << 16 |
+                     (uint64_t)(len & 0xffu) << 24;
+                hl = 4;
+            } else {
+                // 64-bit big-endian length: bytes 2..9 = 0, 0, 0, 0, len >> 24 .. len
+                h0 = b0 | (uint64_t)((masked ? 0x80u : 0u) | 127u) << 8 | (uint64_t)(len >> 24) << 48 |
+                     (uint64_t)((len >> 16) & 0xffu) << 56;
+                h1 = (uint64_t)((len >> 8) & 0xffu) | (uint64_t)(len & 0xffu) << 8;
+                hl = 10;
+            }
+            if (masked) {
+                if (hl == 10) h1 |= (uint64_t)key << 16;
+                else h0 |= (uint64_t)key << (8 * hl);
+                hl += 4;
+            }
+            if (lane < hl) w[wp + lane] = (uint8_t)((lane < 8 ? h0 >> (8 * lane) : h1 >> (8 * (lane - 8))) & 0xffu);
+            uint8_t* dst = w + wp + hl;
+            const uint8_t* src = p + a;
+            const uint32_t full = len >> 4;
+            for (uint32_t u = lane; u < full; u += WAVE) {
+                uint4 v = *(const uint4_fu*)(src + 16 * u);
+                v.x ^= key;
+                v.y ^= key;
+                v.z ^= key;
+                v.w ^= key;
+                *(uint4_fu*)(dst + 16 * u) = v;
+            }
+            const uint32_t t = 16 * full + lane;
+            if (t < len) dst[t] = src[t] ^ (uint8_t)(key >> (8 * (t & 3u)));
+            wp += hl + len;
+        }
+    }
+}
+
 }  // namespace frame
 }  // namespace bpmd
 
@@ -250,5 +329,16 @@ extern "C" int bpmd_internal_slide(uint8_t* buf, const uint64_t* base, const uin
     if (n == 0) return 0;
     hipLaunchKernelGGL(bpmd::frame::slide_kernel, dim3(frame_grid(n)), dim3(bpmd::frame::WAVE * bpmd::frame::WPB), 0,
                        stream, buf, base, pos, keep, n);
+    return (int)hipGetLastError();
+}
+
+extern "C" int bpmd_internal_frame(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint8_t* op,
+                                   const uint8_t* flags, const uint32_t* keys, const uint32_t* key_base,
+                                   uint32_t frame_max, uint32_t n, uint8_t* wire, const uint64_t* wire_off,
+                                   hipStream_t stream)
+{
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(bpmd::frame::frame_kernel, dim3(frame_grid(n)), dim3(bpmd::frame::WAVE * bpmd::frame::WPB), 0,
+                       stream, in, in_off, in_len, op, flags, keys, key_base, frame_max, n, wire, wire_off);
     return (int)hipGetLastError();
 }

@@ -65,6 +65,9 @@ def lib():
         u32 = ctypes.c_uint32
         L.bpmd_mask_batch.argtypes = [vp, vp, vp, u32, vp, vp, vp]
         L.bpmd_utf8_check_batch.argtypes = [vp, vp, vp, u32, vp, vp]
+        L.bpmd_frame_wire_size.argtypes = [ctypes.c_uint64, u32, ctypes.c_int]
+        L.bpmd_frame_wire_size.restype = ctypes.c_uint64
+        L.bpmd_frame_batch.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32, u32, vp, vp, vp]
         L.bpmd_read_batch.argtypes = [ctypes.POINTER(_Cfg), vp, vp, vp, vp, vp, u32, vp, vp, vp, vp, vp, vp]
         L.bpmd_write_batch.argtypes = [ctypes.POINTER(_Cfg), vp, vp, vp, vp, u32, vp, vp, vp, vp, vp, vp]
         L.bpmd_inflate_takeover_batch.argtypes = [ctypes.POINTER(_Cfg), vp, vp, vp, vp, u32, vp, vp, vp, vp, vp, vp]
@@ -259,6 +262,58 @@ def mask_batch(b: Batch, key, phase=None, stream=None) -> None:
     ph = _u8(phase, b.n, dev)
     _check(L.bpmd_mask_batch(_ptr(b.data), _ptr(b.off), _ptr(b.len), b.n, _optr(k), _optr(ph),
                              _stream_handle(stream)), "bpmd_mask_batch")
+
+
+def frame_counts(lens: torch.Tensor, frame_max: int) -> torch.Tensor:
+    """Frames per message (an empty payload is one empty frame)."""
+    lens = lens.to(torch.int64)
+    return torch.clamp((lens + frame_max - 1) // frame_max, min=1)
+
+
+def frame_wire_sizes(lens: torch.Tensor, frame_max: int, masked: bool) -> torch.Tensor:
+    """bpmd_frame_wire_size per message, on the lengths' device."""
+    lens = lens.to(torch.int64)
+    k = frame_counts(lens, frame_max)
+    last = lens - (k - 1) * frame_max
+    hdr = lambda x: torch.where(x <= 125, 2, torch.where(x <= 65535, 4, 10)) + (4 if masked else 0)  # noqa: E731
+    full = torch.full_like(lens, frame_max)
+    return lens + (k - 1) * hdr(full) + hdr(last)
+
+
+def frame_batch(b: Batch, frame_max: int = 4096, op=2, compressed=True, keys: torch.Tensor | None = None,
+                stream=None) -> Batch:
+    """The wire bytes of every message of `b` (write.hpp:463-545 frame loop,
+    frame.hpp:134-175 headers): frames of at most frame_max payload bytes,
+    opcode `op` (per message or one value) and RSV1 when `compressed` on the
+    first frame, FIN on the last; `keys` (client role) holds one key per
+    frame, message by message (frame_counts gives how many), and masks each
+    frame with its own key.  Returns the frames as a Batch of one wire
+    message per input message."""
+    L = lib()
+    dev = b.data.device
+    n = b.n
+    masked = keys is not None
+    sizes = frame_wire_sizes(b.len, frame_max, masked)
+    woff = torch.zeros(n, dtype=torch.int64, device=dev)
+    if n > 1:
+        woff[1:] = torch.cumsum(sizes, 0)[:-1]
+    total = int(sizes.sum().item()) if n else 0
+    wire = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+    opt = _u8(op, n, dev)
+    fl = _u8(1 if compressed is True else 0 if compressed is False else compressed, n, dev)
+    kt = kb = None
+    if masked:
+        cnt = frame_counts(b.len, frame_max)
+        nk = int(keys.numel()) if isinstance(keys, torch.Tensor) else len(keys)
+        kt = _keys(keys, nk, dev)
+        if kt.numel() < int(cnt.sum().item()):
+            raise BpmdError("frame_batch: keys must hold one key per frame (frame_counts)")
+        kb = torch.zeros(n, dtype=torch.int32, device=dev)
+        if n > 1:
+            kb[1:] = torch.cumsum(cnt, 0)[:-1].to(torch.int32)
+    _check(L.bpmd_frame_batch(_ptr(b.data), _ptr(b.off), _ptr(b.len), _optr(opt), _optr(fl), _optr(kt), _optr(kb),
+                              frame_max, n, _ptr(wire), _ptr(woff), _stream_handle(stream)), "bpmd_frame_batch")
+    return Batch(wire, woff, sizes.to(torch.int32))
 
 
 def utf8_check_batch(b: Batch, stream=None, result: torch.Tensor | None = None) -> torch.Tensor:

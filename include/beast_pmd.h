@@ -183,6 +183,24 @@ int bpmd_write_batch(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d
                      const uint32_t* d_key, uint32_t n_msgs, uint8_t* d_out, const uint64_t* d_out_off,
                      const uint32_t* d_out_cap, uint32_t* d_out_len, int32_t* d_status, void* stream);
 
+/* Frames of a batch of messages on the send side, as write_some sends a
+ * compressed message (websocket/impl/write.hpp:463-545) with headers written
+ * by detail::write (websocket/detail/frame.hpp:134-175): message i's payload
+ * d_in + d_in_off[i] (d_in_len[i] bytes, e.g. bpmd_deflate_batch's output)
+ * goes out in frames of at most frame_max bytes (Beast's wr_buf_size; one
+ * empty frame for an empty payload).  Frame f: FIN on the last, RSV1 on the
+ * first when d_flags[i] & 1 (compressed; NULL = all compressed), opcode
+ * d_op[i] on the first (NULL = binary, 2) and cont (0) after; with d_keys
+ * (client role) the MASK bit, key d_keys[d_key_base[i] + f] in the header
+ * (little-endian) and the frame's payload masked with it (a fresh
+ * prepare_key per frame).  The wire bytes go to d_wire + d_wire_off[i];
+ * bpmd_frame_wire_size gives their count.  Any split is a valid RFC 6455
+ * message; Beast's own split also depends on when its deflater flushes. */
+uint64_t bpmd_frame_wire_size(uint64_t payload_len, uint32_t frame_max, int masked);
+int bpmd_frame_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint32_t* d_in_len, const uint8_t* d_op,
+                     const uint8_t* d_flags, const uint32_t* d_keys, const uint32_t* d_key_base, uint32_t frame_max,
+                     uint32_t n_msgs, uint8_t* d_wire, const uint64_t* d_wire_off, void* stream);
+
 /* ---------------------------------------------------------------------
  * Context takeover: when no_context_takeover is not
  * negotiated, Beast's inflater keeps its window from message to message

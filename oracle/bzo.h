@@ -124,6 +124,11 @@ int bzo_pmd_inflate_batch(int window_bits, int raw, const uint8_t* in,
 /* mask_inplace (websocket/detail/mask.ipp:38-59) with a key already rotated
  * by `phase` bytes; returns the rotation afterwards */
 unsigned bzo_mask(uint8_t* p, size_t n, uint32_t key, unsigned phase);
+/* frame headers (websocket/detail/frame.hpp:134-175) and the frame loop of a
+ * message (websocket/impl/write.hpp:463-545); keys NULL = unmasked */
+size_t bzo_frame_wire_size(uint64_t n, uint64_t frame_max, int masked);
+size_t bzo_frame_write(uint8_t* out, const uint8_t* payload, uint64_t n, unsigned op, int rsv1, const uint32_t* keys,
+                       uint64_t frame_max);
 /* utf8_checker (websocket/detail/utf8_checker.hpp/.ipp) */
 typedef struct bzo_utf8 {
     size_t need;   /* bytes still needed by the open code point */

@@ -5,6 +5,11 @@
  *
  * Restates
  *   websocket/detail/mask.ipp:20-59            prepare_key, rol, mask_inplace
+ *   websocket/detail/frame.hpp:134-175         write(DynamicBuffer&, frame_header)
+ *   websocket/impl/write.hpp:463-545           the compressed-message frame loop
+ *                                               (op / rsv1 on the first frame,
+ *                                               cont after, fin on the last,
+ *                                               a key per frame)
  *   websocket/detail/utf8_checker.ipp:22-324   utf8_checker::reset / finish /
  *                                               write, check_utf8
  * The checker is restated by its rules rather than its loops: the
@@ -16,7 +21,8 @@
  * Pinned by the expectations of the reference's own tests
  * (test/beast/websocket/utf8_checker.cpp, restated as data in
  * tests/utf8_cases.py), by CPython's UTF-8 decoder on random input
- * (tests/test_frame.py) and, for masking, by RFC 6455 §5.7's example frame.
+ * (tests/test_frame.py) and, for masking and frame headers, by the example
+ * frames of RFC 6455 §5.7 and RFC 7692 §7.2.3 (tests/test_frame.py).
  */
 #include <string.h>
 
@@ -132,4 +138,62 @@ int bzo_utf8_check_batch(const uint8_t* in, const uint64_t* off, const uint32_t*
 {
     for (uint32_t i = 0; i < n; ++i) result[i] = bzo_utf8_check(in + off[i], len[i]);
     return 0;
+}
+
+/* frame.hpp:134-175: FIN | RSV1 | opcode, MASK | 7-bit length (126: 16-bit,
+ * 127: 64-bit big-endian), then the key in little-endian byte order */
+static size_t frame_header(uint8_t* b, int fin, int rsv1, unsigned op, int mask, uint64_t len, uint32_t key)
+{
+    size_t n;
+    b[0] = (uint8_t)((fin ? 0x80u : 0u) | (rsv1 ? 0x40u : 0u) | (op & 15u));
+    b[1] = mask ? 0x80u : 0u;
+    if (len <= 125) {
+        b[1] |= (uint8_t)len;
+        n = 2;
+    } else if (len <= 65535) {
+        b[1] |= 126;
+        b[2] = (uint8_t)(len >> 8);
+        b[3] = (uint8_t)len;
+        n = 4;
+    } else {
+        b[1] |= 127;
+        for (int i = 0; i < 8; ++i) b[2 + i] = (uint8_t)(len >> (8 * (7 - i)));
+        n = 10;
+    }
+    if (mask) {
+        for (int i = 0; i < 4; ++i) b[n + i] = (uint8_t)(key >> (8 * i));
+        n += 4;
+    }
+    return n;
+}
+
+size_t bzo_frame_wire_size(uint64_t n, uint64_t frame_max, int masked)
+{
+    const uint64_t frames = n == 0 ? 1 : (n + frame_max - 1) / frame_max;
+    size_t total = (size_t)n;
+    for (uint64_t f = 0; f < frames; ++f) {
+        const uint64_t len = f + 1 < frames ? frame_max : n - f * frame_max;
+        total += (len <= 125 ? 2 : len <= 65535 ? 4 : 10) + (masked ? 4 : 0);
+    }
+    return total;
+}
+
+/* write.hpp:463-545: the payload goes out in frames of at most frame_max
+ * bytes (the wr_buf the deflater fills); the first frame carries the opcode
+ * and RSV1 (a compressed message), later ones opcode cont (0) and no RSV1;
+ * FIN on the last; a client masks each frame with its own key (keys[f]). */
+size_t bzo_frame_write(uint8_t* out, const uint8_t* payload, uint64_t n, unsigned op, int rsv1, const uint32_t* keys,
+                       uint64_t frame_max)
+{
+    const uint64_t frames = n == 0 ? 1 : (n + frame_max - 1) / frame_max;
+    size_t w = 0;
+    for (uint64_t f = 0; f < frames; ++f) {
+        const uint64_t a = f * frame_max, len = f + 1 < frames ? frame_max : n - a;
+        const uint32_t key = keys ? keys[f] : 0u;
+        w += frame_header(out + w, f + 1 == frames, f == 0 && rsv1, f == 0 ? op : 0u, keys != NULL, len, key);
+        memcpy(out + w, payload + a, (size_t)len);
+        if (keys) bzo_mask(out + w, (size_t)len, key, 0);
+        w += (size_t)len;
+    }
+    return w;
 }

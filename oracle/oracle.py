@@ -70,6 +70,11 @@ def lib():
         L.bzo_pmd_inflate_batch.argtypes = [ctypes.c_int, ctypes.c_int] + [vp] * 3 + [ctypes.c_uint32] + [vp] * 5 + [ctypes.c_int]
         L.bzo_mask.argtypes = [vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint]
         L.bzo_mask.restype = ctypes.c_uint
+        L.bzo_frame_wire_size.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int]
+        L.bzo_frame_wire_size.restype = ctypes.c_size_t
+        L.bzo_frame_write.argtypes = [vp, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint, ctypes.c_int, vp,
+                                      ctypes.c_uint64]
+        L.bzo_frame_write.restype = ctypes.c_size_t
         L.bzo_utf8_reset.argtypes = [vp]
         L.bzo_utf8_write.argtypes = [vp, ctypes.c_char_p, ctypes.c_size_t]
         L.bzo_utf8_finish.argtypes = [vp]
@@ -276,6 +281,24 @@ def mask(data: bytes, key: int, phase: int = 0) -> bytes:
     buf = ctypes.create_string_buffer(data, max(len(data), 1))
     lib().bzo_mask(buf, len(data), key & 0xFFFFFFFF, phase & 3)
     return buf.raw[:len(data)]
+
+
+def frame_write(payload: bytes, op: int, rsv1: bool, keys=None, frame_max: int = 4096) -> bytes:
+    """A message's frames on the wire (frame.hpp:134-175 headers, the
+    write.hpp:463-545 frame loop): frames of at most frame_max payload bytes,
+    opcode and RSV1 on the first, FIN on the last, frame f masked with keys[f]
+    (None = unmasked)."""
+    payload = bytes(payload)
+    L = lib()
+    masked = keys is not None
+    size = L.bzo_frame_wire_size(len(payload), frame_max, int(masked))
+    out = ctypes.create_string_buffer(max(size, 1))
+    kp = None
+    if masked:
+        kp = (ctypes.c_uint32 * max(len(keys), 1))(*[k & 0xFFFFFFFF for k in keys])
+    w = L.bzo_frame_write(out, payload, len(payload), op, int(bool(rsv1)), kp, frame_max)
+    assert w == size
+    return out.raw[:w]
 
 
 def utf8_check(data: bytes) -> int:

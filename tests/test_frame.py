@@ -135,3 +135,44 @@ def test_frame_entry_points_validate_before_device_use():
     assert L.bpmd_inflate_takeover_batch(ctypes.byref(cfg), None, None, None, None, 1, None, None, None, None, None,
                                          None) == -1
     assert L.bpmd_slide_batch(None, None, None, None, 1, None) == -1
+    assert L.bpmd_frame_batch(None, None, None, None, None, None, None, 4096, 0, None, None, None) == 0
+    assert L.bpmd_frame_batch(None, None, None, None, None, None, None, 4096, 1, None, None, None) == -1
+
+
+# RFC 6455 §5.7 and RFC 7692 §7.2.3 example frames: the header layout that
+# websocket/detail/frame.hpp:134-175 writes (key little-endian on the wire)
+_HELLO_DEFLATED = bytes([0xf2, 0x48, 0xcd, 0xc9, 0xc9, 0x07, 0x00])
+
+
+def test_frame_headers_rfc_examples():
+    assert O.frame_write(b"Hello", 1, False) == bytes([0x81, 0x05]) + b"Hello"
+    assert O.frame_write(b"Hello", 1, False, keys=[0x3d21fa37]) == bytes(
+        [0x81, 0x85, 0x37, 0xfa, 0x21, 0x3d, 0x7f, 0x9f, 0x4d, 0x51, 0x58])
+    assert O.frame_write(b"Hello", 1, False, frame_max=3) == bytes([0x01, 0x03]) + b"Hel" + bytes([0x80, 0x02]) + b"lo"
+    f = O.frame_write(bytes(256), 2, False)
+    assert f[:4] == bytes([0x82, 0x7e, 0x01, 0x00]) and len(f) == 260
+    f = O.frame_write(bytes(65536), 2, False, frame_max=1 << 20)
+    assert f[:10] == bytes([0x82, 0x7f, 0, 0, 0, 0, 0, 1, 0, 0]) and len(f) == 65546
+    # permessage-deflate: RSV1 on the first frame only
+    assert O.frame_write(_HELLO_DEFLATED, 1, True) == bytes([0xc1, 0x07]) + _HELLO_DEFLATED
+    f = O.frame_write(_HELLO_DEFLATED, 1, True, frame_max=3)
+    assert f == bytes([0x41, 0x03]) + _HELLO_DEFLATED[:3] + bytes([0x00, 0x03]) + _HELLO_DEFLATED[3:6] + \
+        bytes([0x80, 0x01]) + _HELLO_DEFLATED[6:]
+    assert O.frame_write(b"", 2, True) == bytes([0xc2, 0x00])
+
+
+def test_frame_wire_size_matches_oracle():
+    import torch
+    L = pmd.lib()
+    rng = random.Random(16)
+    lens = [0, 1, 124, 125, 126, 127, 4095, 4096, 4097, 65535, 65536, 65537, 200000] + \
+        [rng.randrange(0, 300000) for _ in range(40)]
+    for fm in (1, 3, 125, 126, 4096, 65535, 65536, 1 << 20):
+        for masked in (0, 1):
+            want = [len(O.frame_write(bytes(n), 2, True, keys=[0] * (max(1, -(-n // fm))) if masked else None,
+                                      frame_max=fm)) for n in lens] if fm >= 125 else None
+            got = [L.bpmd_frame_wire_size(n, fm, masked) for n in lens]
+            if want is not None:
+                assert got == want, (fm, masked)
+            t = pmd.frame_wire_sizes(torch.tensor(lens), fm, bool(masked)).tolist()
+            assert t == got, (fm, masked)

@@ -179,3 +179,76 @@ def test_write_batch_masks_the_deflate_payloads():
         assert O.mask(ms[i], keys[i]) == pl[i], i
         st, out = O.pmd_inflate(pl[i], cap=max(len(msgs[i]), 1))
         assert st == 0 and out == msgs[i]
+
+
+@pytest.mark.parametrize("frame_max", [125, 126, 4096, 65536, 1 << 20])
+def test_frame_batch_matches_oracle(frame_max):
+    """bpmd_frame_batch's wire bytes equal the oracle's frame loop
+    (write.hpp:463-545, frame.hpp:134-175), masked and unmasked, with
+    per-message opcodes and RSV1 flags, ragged lengths and 7/16/64-bit
+    frame lengths."""
+    import torch
+    pmd = _pmd()
+    rng = random.Random(17 + frame_max)
+    lens = [0, 1, 3, 15, 16, 17, 125, 126, 127, 4095, 4096, 4097, 65535, 65536, 70001] + \
+        [rng.randrange(0, 9000) for _ in range(150)]
+    msgs = [rng.randbytes(n) for n in lens]
+    ops = [rng.choice([1, 2]) for _ in msgs]
+    comp = [rng.choice([0, 1]) for _ in msgs]
+    src = pmd.Batch.from_host(msgs)
+    for masked in (False, True):
+        cnt = pmd.frame_counts(src.len, frame_max).tolist()
+        keys = [rng.getrandbits(32) for _ in range(sum(cnt))] if masked else None
+        wire = pmd.frame_batch(src, frame_max, op=torch.tensor(ops, dtype=torch.uint8),
+                               compressed=torch.tensor(comp, dtype=torch.uint8), keys=keys)
+        torch.cuda.synchronize()
+        got = wire.to_host()
+        k0 = 0
+        for i, m in enumerate(msgs):
+            ks = keys[k0:k0 + cnt[i]] if masked else None
+            k0 += cnt[i]
+            assert got[i] == O.frame_write(m, ops[i], bool(comp[i]), keys=ks, frame_max=frame_max), (i, masked)
+
+
+def test_write_then_frame_round_trip():
+    """Send path end to end: GPU deflate, GPU framing with client keys; the
+    frames parsed and unmasked on the host give back the payloads, and the
+    payloads inflate (oracle) to the messages."""
+    import torch
+    pmd = _pmd()
+    rng = random.Random(18)
+    msgs = []
+    for i in range(200):
+        d, _, _ = synth.make_batch(rng.choice(["json", "binary"]), [rng.choice([0, 10, 4096, 9000, 30000])], seed=i)
+        msgs.append(bytes(d))
+    src = pmd.Batch.from_host(msgs)
+    payloads = pmd.deflate_batch(src, level=6)
+    assert payloads.status.cpu().tolist() == [0] * len(msgs)
+    pb = payloads.out
+    cnt = pmd.frame_counts(pb.len, 4096).tolist()
+    keys = [rng.getrandbits(32) for _ in range(sum(cnt))]
+    wire = pmd.frame_batch(pb, 4096, op=1, compressed=True, keys=keys).to_host()
+    torch.cuda.synchronize()
+    k0 = 0
+    for i, w in enumerate(wire):
+        # parse: header, key, unmask, concatenate
+        pos, out, first = 0, b"", True
+        while True:
+            b0, b1 = w[pos], w[pos + 1]
+            assert (b0 & 0x0F) == (1 if first else 0) and bool(b0 & 0x40) == first and b1 & 0x80
+            ln, pos = b1 & 0x7F, pos + 2
+            if ln == 126:
+                ln, pos = int.from_bytes(w[pos:pos + 2], "big"), pos + 2
+            elif ln == 127:
+                ln, pos = int.from_bytes(w[pos:pos + 8], "big"), pos + 8
+            key = int.from_bytes(w[pos:pos + 4], "little")
+            assert key == keys[k0]
+            k0, pos = k0 + 1, pos + 4
+            out += O.mask(w[pos:pos + ln], key)
+            pos += ln
+            first = False
+            if b0 & 0x80:
+                break
+        assert pos == len(w)
+        st, plain = O.pmd_inflate(out, cap=max(len(msgs[i]), 1))
+        assert st == 0 and plain == msgs[i], i
