@@ -280,40 +280,58 @@ def frame_wire_sizes(lens: torch.Tensor, frame_max: int, masked: bool) -> torch.
     return lens + (k - 1) * hdr(full) + hdr(last)
 
 
-def frame_batch(b: Batch, frame_max: int = 4096, op=2, compressed=True, keys: torch.Tensor | None = None,
-                stream=None) -> Batch:
-    """The wire bytes of every message of `b` (write.hpp:463-545 frame loop,
-    frame.hpp:134-175 headers): frames of at most frame_max payload bytes,
-    opcode `op` (per message or one value) and RSV1 when `compressed` on the
-    first frame, FIN on the last; `keys` (client role) holds one key per
-    frame, message by message (frame_counts gives how many), and masks each
-    frame with its own key.  Returns the frames as a Batch of one wire
-    message per input message."""
-    L = lib()
+def frame_plan(b: Batch, frame_max: int = 4096, masked: bool = False):
+    """Wire sizes, wire offsets, total bytes and (masked) each message's first
+    key index for bpmd_frame_batch; reusable across calls on same-shaped batches."""
     dev = b.data.device
     n = b.n
-    masked = keys is not None
     sizes = frame_wire_sizes(b.len, frame_max, masked)
     woff = torch.zeros(n, dtype=torch.int64, device=dev)
     if n > 1:
         woff[1:] = torch.cumsum(sizes, 0)[:-1]
     total = int(sizes.sum().item()) if n else 0
-    wire = torch.empty(total + 16, dtype=torch.uint8, device=dev)
-    opt = _u8(op, n, dev)
-    fl = _u8(1 if compressed is True else 0 if compressed is False else compressed, n, dev)
-    kt = kb = None
+    kb = nkeys = None
     if masked:
         cnt = frame_counts(b.len, frame_max)
-        nk = int(keys.numel()) if isinstance(keys, torch.Tensor) else len(keys)
-        kt = _keys(keys, nk, dev)
-        if kt.numel() < int(cnt.sum().item()):
-            raise BpmdError("frame_batch: keys must hold one key per frame (frame_counts)")
+        nkeys = int(cnt.sum().item())
         kb = torch.zeros(n, dtype=torch.int32, device=dev)
         if n > 1:
             kb[1:] = torch.cumsum(cnt, 0)[:-1].to(torch.int32)
-    _check(L.bpmd_frame_batch(_ptr(b.data), _ptr(b.off), _ptr(b.len), _optr(opt), _optr(fl), _optr(kt), _optr(kb),
-                              frame_max, n, _ptr(wire), _ptr(woff), _stream_handle(stream)), "bpmd_frame_batch")
-    return Batch(wire, woff, sizes.to(torch.int32))
+    return {"frame_max": frame_max, "masked": masked, "sizes": sizes.to(torch.int32), "woff": woff, "total": total,
+            "key_base": kb, "n_keys": nkeys}
+
+
+def frame_batch(b: Batch, frame_max: int = 4096, op=2, compressed=True, keys=None, stream=None, plan=None,
+                wire: torch.Tensor | None = None) -> Batch:
+    """The wire bytes of every message of `b` (write.hpp:463-545 frame loop,
+    frame.hpp:134-175 headers): frames of at most frame_max payload bytes,
+    opcode `op` (per message or one value) and RSV1 when `compressed` on the
+    first frame, FIN on the last; `keys` (client role) holds one key per
+    frame, message by message (frame_counts gives how many), and masks each
+    frame with its own key.  Returns one wire message per input message;
+    `plan` (frame_plan) and `wire` skip the sizing and allocation."""
+    L = lib()
+    dev = b.data.device
+    n = b.n
+    masked = keys is not None
+    if plan is None:
+        plan = frame_plan(b, frame_max, masked)
+    if plan["frame_max"] != frame_max or plan["masked"] != masked:
+        raise BpmdError("frame_batch: plan made for another frame size or role")
+    if wire is None:
+        wire = torch.empty(plan["total"] + 16, dtype=torch.uint8, device=dev)
+    opt = _u8(op, n, dev)
+    fl = _u8(1 if compressed is True else 0 if compressed is False else compressed, n, dev)
+    kt = None
+    if masked:
+        nk = int(keys.numel()) if isinstance(keys, torch.Tensor) else len(keys)
+        kt = _keys(keys, nk, dev)
+        if kt.numel() < plan["n_keys"]:
+            raise BpmdError("frame_batch: keys must hold one key per frame (frame_counts)")
+    _check(L.bpmd_frame_batch(_ptr(b.data), _ptr(b.off), _ptr(b.len), _optr(opt), _optr(fl), _optr(kt),
+                              _optr(plan["key_base"]), frame_max, n, _ptr(wire), _ptr(plan["woff"]),
+                              _stream_handle(stream)), "bpmd_frame_batch")
+    return Batch(wire, plan["woff"], plan["sizes"])
 
 
 def utf8_check_batch(b: Batch, stream=None, result: torch.Tensor | None = None) -> torch.Tensor:
