@@ -57,7 +57,10 @@ constexpr unsigned O_NIB = 448;    // u8[160]  code lengths, one nibble per symb
 constexpr unsigned O_HEAD = 624;   // u32      tokens written (decoder)
 constexpr unsigned O_TAIL = 628;   // u32      tokens taken (expander)
 constexpr unsigned STRIDE = 632;   // x 64 lanes x 4 workgroups = 161 792 B per CU
-constexpr unsigned RING = 32;
+#ifndef BPMD3_RING
+#define BPMD3_RING 32
+#endif
+constexpr unsigned RING = BPMD3_RING;   // token ring entries per message (at most 32: the header scratch holds 32)
 constexpr unsigned WG_MSGS = 64;
 constexpr uint32_t TOK_END = 0x80000000u;   // word 0: out_len, bits 0-7: status
 constexpr uint32_t TOK_NEW = 0x40000000u;   // word 0: the message the lane starts (work queue)
