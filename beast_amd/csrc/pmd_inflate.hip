@@ -1016,19 +1016,12 @@ inflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
                const uint32_t* __restrict__ in_len, uint32_t n_msgs, uint8_t* __restrict__ out,
                const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
                uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t raw,
-               const uint32_t* __restrict__ mask_key, uint32_t min_in, bpmd_resume_call rc)
+               const uint32_t* __restrict__ mask_key, uint32_t min_in, bpmd_resume_call rc,
+               uint32_t* __restrict__ qctr)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     WaveLds& L = *reinterpret_cast<WaveLds*>(smem);
-    // the wave's messages are blockIdx.x + k * gridDim.x; their lengths are
-    // read 64 at a time (one per lane) so skipping costs no serial loads.
-    // min_in != 0: only payloads longer than min_in (the lane kernel has the rest)
-    for (uint64_t first = blockIdx.x; first < n_msgs; first += (uint64_t)WAVE * gridDim.x) {
-    const uint64_t mine = first + (uint64_t)lane_id() * gridDim.x;
-    uint64_t todo = __ballot(mine < n_msgs && (!min_in || in_len[mine] > min_in));
-    while (todo) {
-        const uint32_t msg = (uint32_t)(first + (uint64_t)__builtin_ctzll(todo) * gridDim.x);
-        todo &= todo - 1;
+    auto run = [&](uint32_t msg) {
         Msg m;
         m.p = in + in_off[msg];
         m.n = in_len[msg];
@@ -1047,6 +1040,31 @@ inflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
             status[msg] = st;
         }
         wave_sync();
+    };
+    if (qctr) {
+        // work queue: a wave takes the next message when its last one is
+        // done, so waves that share a SIMD with more waves (9 per CU on 4
+        // SIMDs) take fewer messages instead of setting the launch's end
+        for (;;) {
+            uint32_t k = 0;
+            if (lane_id() == 0) k = atomicAdd(qctr, 1u);
+            k = (uint32_t)__builtin_amdgcn_readfirstlane((int)k);
+            if (k >= n_msgs) break;
+            if (min_in && in_len[k] <= min_in) continue;
+            run(k);
+        }
+        return;
+    }
+    // the wave's messages are blockIdx.x + k * gridDim.x; their lengths are
+    // read 64 at a time (one per lane) so skipping costs no serial loads.
+    // min_in != 0: only payloads longer than min_in (the lane kernel has the rest)
+    for (uint64_t first = blockIdx.x; first < n_msgs; first += (uint64_t)WAVE * gridDim.x) {
+    const uint64_t mine = first + (uint64_t)lane_id() * gridDim.x;
+    uint64_t todo = __ballot(mine < n_msgs && (!min_in || in_len[mine] > min_in));
+    while (todo) {
+        const uint32_t msg = (uint32_t)(first + (uint64_t)__builtin_ctzll(todo) * gridDim.x);
+        todo &= todo - 1;
+        run(msg);
     }
     }
 }
@@ -1056,6 +1074,10 @@ inflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
 // ---------------------------------------------------------------- launcher
 
 extern "C" unsigned bpmd_diag_grid_override;   // pmd_capi.hip; 0 = size the grid by occupancy
+extern "C" void* bpmd_internal_scratch(hipStream_t s, size_t bytes, int which);
+#ifndef BPMD_WAVE_QUEUE
+#define BPMD_WAVE_QUEUE 1
+#endif
 
 extern "C" int bpmd_internal_inflate_keyed_split(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                            uint32_t n, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
@@ -1071,8 +1093,14 @@ extern "C" int bpmd_internal_inflate_keyed_split(const uint8_t* in, const uint64
     unsigned grid = (unsigned)cus * (per_cu ? per_cu : 1);
     if (bpmd_diag_grid_override) grid = bpmd_diag_grid_override;
     if (grid > n) grid = n;
+    // more messages than resident waves: a work queue (scratch block 6)
+    uint32_t* qctr = nullptr;
+    if (BPMD_WAVE_QUEUE && n > grid) {
+        qctr = (uint32_t*)bpmd_internal_scratch(stream, 256, 6);
+        if (!qctr || hipMemsetAsync(qctr, 0, sizeof(uint32_t), stream) != hipSuccess) return (int)hipErrorOutOfMemory;
+    }
     hipLaunchKernelGGL(inflate_kernel<false>, dim3(grid), dim3(WAVE), lds, stream, in, in_off, in_len, n, out,
-                       out_off, out_cap, out_len, status, raw, mask_key, min_in, bpmd_resume_call{});
+                       out_off, out_cap, out_len, status, raw, mask_key, min_in, bpmd_resume_call{}, qctr);
     return (int)hipGetLastError();
 }
 
@@ -1085,7 +1113,7 @@ extern "C" int bpmd_internal_inflate_resume(const uint8_t* in, const uint64_t* i
 {
     using namespace bpmd;
     hipLaunchKernelGGL(inflate_kernel<true>, dim3(1), dim3(WAVE), sizeof(WaveLds), stream, in, in_off, in_len, 1u,
-                       out, out_off, out_cap, out_len, status, 1u, nullptr, 0u, rc);
+                       out, out_off, out_cap, out_len, status, 1u, nullptr, 0u, rc, (uint32_t*)nullptr);
     return (int)hipGetLastError();
 }
 
