@@ -1164,12 +1164,20 @@ __global__ void __launch_bounds__(64)
 deflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint32_t* __restrict__ in_len,
                uint32_t n, uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
                const uint32_t* __restrict__ out_cap, uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
-               Params P)
+               Params P, uint32_t* __restrict__ qctr)
 {
     __shared__ DefLds<0> S;
     const unsigned lane = lane_id();
     Prof pf;
-    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    // messages from a counter when the batch outnumbers the waves (a wave
+    // whose messages were short takes more), a fixed stride otherwise
+    auto next = [&](uint32_t i) -> uint32_t {
+        if (!qctr) return i + gridDim.x;
+        uint32_t v = 0;
+        if (lane == 0) v = atomicAdd(qctr, 1u);
+        return gridDim.x + (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+    };
+    for (uint32_t i = blockIdx.x; i < n; i = next(i)) {
         const uint32_t len = in_len[i];
         if (len > CHUNK) continue;   // chunk-parallel path (deflate_chunks_kernel + stitch_kernel)
         MsgOut o;
@@ -1363,9 +1371,13 @@ stitch_kernel(const uint32_t* __restrict__ in_len, uint32_t n, uint32_t all, con
 
 extern "C" unsigned bpmd_diag_grid_override;
 extern "C" void* bpmd_internal_scratch(hipStream_t s, size_t bytes, int which);
+#ifndef BPMD_DEFLATE_QUEUE
+#define BPMD_DEFLATE_QUEUE 1
+#endif
 
 namespace {
-// single-chunk messages: as many waves as the LDS holds, grid-strided
+// single-chunk messages: as many waves as the LDS holds, grid-strided or
+// (BPMD_DEFLATE_QUEUE) drained from a counter
 int launch_single(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n, uint8_t* out,
                   const uint64_t* out_off, const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
                   const bpmd::dfl::Params& P, hipStream_t stream)
@@ -1376,8 +1388,13 @@ int launch_single(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_
     unsigned grid = (unsigned)cus * (per_cu ? per_cu : 1u);
     if (bpmd_diag_grid_override) grid = bpmd_diag_grid_override;
     if (grid > n) grid = n;
+    uint32_t* qctr = nullptr;
+    if (BPMD_DEFLATE_QUEUE && n > grid) {   // scratch block 7: the single-chunk message counter
+        qctr = (uint32_t*)bpmd_internal_scratch(stream, 256, 7);
+        if (!qctr || hipMemsetAsync(qctr, 0, sizeof(uint32_t), stream) != hipSuccess) return (int)hipErrorOutOfMemory;
+    }
     hipLaunchKernelGGL(bpmd::dfl::deflate_kernel, dim3(grid), dim3(64), 0, stream, in, in_off, in_len, n, out, out_off,
-                       out_cap, out_len, status, P);
+                       out_cap, out_len, status, P, qctr);
     return (int)hipGetLastError();
 }
 }  // namespace
