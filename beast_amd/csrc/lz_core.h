@@ -50,17 +50,18 @@ LZ_HD Level level_params(int level)
 }
 
 // Chain limit the GPU encoder uses: the level table's, capped at
-// BPMD_CHAIN_CAP for messages of one 4 KiB chunk (C3 corpus at level 6, round
-// 2 build: cap 4 / 8 / 16 = 37.5 / 33.9 / 30.0 GiB/s at 1.056 / 1.038 / 1.020x
-// Beast's size) and at BPMD_CHAIN_CAP_MULTI (0 = the table's
-// value) for the chunks of longer messages, which see BPMD_CHUNK_HIST bytes of
-// history before the chunk.  configs[3] (C4), whole batch, size against Beast
-// at level 6 and deflate GiB/s:
+// BPMD_CHAIN_CAP for messages of one 4 KiB chunk (C3 corpus at level 6, final
+// round-2 build with the message queue: cap 8 / 12 / 16 = 37.4 / 35.0 / 33.1
+// GiB/s at 1.038 / 1.028 / 1.020x Beast's size; 16 is the
+// default) and at BPMD_CHAIN_CAP_MULTI (0 = the table's value) for the chunks
+// of longer messages, which see BPMD_CHUNK_HIST bytes of history before the
+// chunk.  configs[3] (C4), whole batch, size against Beast at level 6 and
+// deflate GiB/s:
 //   history 4096, cap 16: 1.086x, 16.4 (the LDS holds 5 waves per CU)
 //   history 2048, cap 16: 1.111x, 23.9 (6 waves per CU)
 //   history 2048, cap 32: 1.089x, 20.9   <- default
 #ifndef BPMD_CHAIN_CAP
-#define BPMD_CHAIN_CAP 8
+#define BPMD_CHAIN_CAP 16
 #endif
 #ifndef BPMD_CHAIN_CAP_MULTI
 #define BPMD_CHAIN_CAP_MULTI 32
