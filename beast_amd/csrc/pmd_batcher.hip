@@ -90,6 +90,8 @@ struct bpmd_batcher {
     std::thread launcher, completer;
 };
 
+extern "C" void bpmd_internal_scratch_release(hipStream_t stream);
+
 namespace {
 
 void free_slot(Slot& s)
@@ -100,7 +102,11 @@ void free_slot(Slot& s)
     for (void* p : {(void*)s.d_in, (void*)s.d_out, (void*)s.d_in_off, (void*)s.d_out_off, (void*)s.d_in_len,
                     (void*)s.d_out_cap, (void*)s.d_out_len, (void*)s.d_status})
         if (p) (void)hipFree(p);
-    if (s.stream) (void)hipStreamDestroy(s.stream);
+    if (s.stream) {
+        (void)hipStreamSynchronize(s.stream);
+        bpmd_internal_scratch_release(s.stream);
+        (void)hipStreamDestroy(s.stream);
+    }
     s = Slot();
 }
 

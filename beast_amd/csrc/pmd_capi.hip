@@ -6,6 +6,7 @@
 
 #include <atomic>
 #include <mutex>
+#include <new>
 #include <vector>
 
 #include "../../include/beast_pmd.h"
@@ -57,9 +58,12 @@ std::mutex g_init_mu;
 int g_init_device = -1;   // device whose symbols are initialised
 
 // Per (device, stream) scratch for batch calls that need device workspace
-// (the inflate work queue's counter and message order).  Allocated on first
-// use and grown when a larger batch arrives; calls on one stream are ordered
-// by the stream, calls on different streams use different scratch.
+// (work-queue counters, message order, chunk workspace).  Allocated on first
+// use and grown when a larger batch arrives.  A batch call holds its
+// stream's launch lock from its first enqueue to its last, so two host
+// threads submitting on one stream (the null stream, say) cannot interleave
+// their memsets and launches over the same counters and workspace; calls on
+// different streams use different scratch.
 struct Scratch {
     int dev;
     hipStream_t stream;
@@ -67,39 +71,103 @@ struct Scratch {
     uint8_t* p;
     size_t cap;
 };
+struct StreamLock {
+    int dev;
+    hipStream_t stream;
+    std::mutex* mu;
+};
 std::mutex g_scratch_mu;
 std::vector<Scratch> g_scratch;
+std::vector<StreamLock> g_locks;
 
-uint8_t* scratch_for(hipStream_t s, size_t bytes, int which = 0)
+std::mutex* stream_mutex(hipStream_t s)
 {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
     std::lock_guard<std::mutex> lk(g_scratch_mu);
-    for (auto& e : g_scratch)
-        if (e.dev == dev && e.stream == s && e.which == which) {
-            if (e.cap >= bytes) return e.p;
-            // the stream may still use the old block: free it once the stream is idle
-            if (hipStreamSynchronize(s) != hipSuccess) return nullptr;
-            (void)hipFree(e.p);
-            e.p = nullptr;
-            e.cap = 0;
-            if (hipMalloc(&e.p, bytes) != hipSuccess) return nullptr;
-            e.cap = bytes;
-            return e.p;
-        }
+    for (auto& e : g_locks)
+        if (e.dev == dev && e.stream == s) return e.mu;
+    std::mutex* mu = new (std::nothrow) std::mutex();
+    if (mu) g_locks.push_back(StreamLock{dev, s, mu});
+    return mu;
+}
+
+// the caller holds the stream's launch lock, so nothing else enqueues work
+// that could use the block while it is replaced
+uint8_t* scratch_for(hipStream_t s, size_t bytes, int which = 0)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    uint8_t* old = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_scratch_mu);
+        for (auto& e : g_scratch)
+            if (e.dev == dev && e.stream == s && e.which == which) {
+                if (e.cap >= bytes) return e.p;
+                old = e.p;
+                e.p = nullptr;
+                e.cap = 0;
+                break;
+            }
+    }
+    // the stream may still use the old block: free it once the stream is idle
+    if (old) {
+        if (hipStreamSynchronize(s) != hipSuccess) return nullptr;
+        (void)hipFree(old);
+    }
     uint8_t* p = nullptr;
     if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    for (auto& e : g_scratch)
+        if (e.dev == dev && e.stream == s && e.which == which) {
+            e.p = p;
+            e.cap = bytes;
+            return p;
+        }
     g_scratch.push_back(Scratch{dev, s, which, p, bytes});
     return p;
 }
 }
 
 // scratch block `which` (0 inflate queue, 1-2 deflate workspace, 3-4 exact
-// deflate queue and workspace, 5 inflate message order, 6 wave inflate queue) for other
-// translation units
+// deflate queue and workspace, 5 inflate message order, 6 wave inflate queue,
+// 7 deflate chunk queue) for other translation units
 extern "C" void* bpmd_internal_scratch(hipStream_t s, size_t bytes, int which)
 {
     return scratch_for(s, bytes, which);
+}
+
+// Frees every scratch block and the launch lock of a stream that is about to
+// be destroyed (per-stream codecs, batcher slots).  The caller has
+// synchronised the stream and no other thread uses it.
+extern "C" void bpmd_internal_scratch_release(hipStream_t s)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return;
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    for (size_t i = 0; i < g_scratch.size();) {
+        if (g_scratch[i].dev == dev && g_scratch[i].stream == s) {
+            (void)hipFree(g_scratch[i].p);
+            g_scratch[i] = g_scratch.back();
+            g_scratch.pop_back();
+        } else {
+            ++i;
+        }
+    }
+    for (size_t i = 0; i < g_locks.size(); ++i)
+        if (g_locks[i].dev == dev && g_locks[i].stream == s) {
+            delete g_locks[i].mu;
+            g_locks[i] = g_locks.back();
+            g_locks.pop_back();
+            break;
+        }
+}
+
+// Number of scratch blocks held (footprint tests)
+extern "C" size_t bpmd_internal_scratch_count(void)
+{
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    return g_scratch.size();
 }
 
 extern "C" const char* bpmd_version(void) { return "beast_pmd 0.2 (gfx950)"; }
@@ -182,6 +250,9 @@ int inflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
     if (r) return r;
     const uint32_t raw = (cfg->flags & BPMD_F_RAW) ? 1u : 0u;
     const hipStream_t s = (hipStream_t)stream;
+    std::mutex* mu = stream_mutex(s);
+    if (!mu) return BPMD_R_HIP_ERROR;
+    std::lock_guard<std::mutex> launch(*mu);
     const int m = inflate_mode();
     // lane-kernel share: everything (hist / forced lane), nothing (forced wave /
     // small batch), or the payloads of at most `split` bytes
@@ -244,6 +315,9 @@ int deflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
         return BPMD_R_INVALID_ARGUMENT;
     int r = bpmd_init();
     if (r) return r;
+    std::mutex* mu = stream_mutex((hipStream_t)stream);
+    if (!mu) return BPMD_R_HIP_ERROR;
+    std::lock_guard<std::mutex> launch(*mu);
     if (cfg->flags & BPMD_F_EXACT) {
         // the reference's own algorithm, message by message (pmd_deflate_exact.hip)
         if (hist) return BPMD_R_INVALID_ARGUMENT;

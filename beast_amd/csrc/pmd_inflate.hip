@@ -37,7 +37,6 @@
 #include "pmd_common.h"
 #include "huff_table.h"
 #include "huff_wave.h"
-#include "inflate_resume.h"
 
 namespace bpmd {
 
@@ -320,28 +319,12 @@ __device__ __forceinline__ LaneRes decode_count(const WaveLds& L, uint32_t wb, u
 // reference makes at each token's output position (inflate_stream.ipp:
 // 475-514): a full buffer first when the capacity is exact (raw), then the
 // distance, then the capacity.
-// Window rule of one decode (inflate_stream.ipp:1046-1061, 475-496): a
-// fresh message may reach back to its own first byte; a per-stream call
-// resumed at a checkpoint follows bpmd_resume_call's rule (inflate_resume.h).
-struct WinRule {
-    uint32_t hist, D, cw;
-};
-
-template <bool RS>
-__device__ __forceinline__ bool dist_bad(uint32_t dist, uint32_t abs, uint32_t olen, uint32_t cap, const WinRule& w)
-{
-    if (!RS) return dist > abs;
-    if (abs >= w.D) return dist > w.cw + (abs - w.D);
-    uint32_t lim = w.hist + abs;
-    const uint32_t stop = abs + olen < cap ? abs + olen : cap;   // the match's output ends there
-    if (stop > w.D && w.cw < lim) lim = w.cw;                    // and continues at this call's start
-    return dist > lim;
-}
-
-template <bool RS>
+// A whole message is decoded in one call from a fresh state, so a distance
+// may reach back to the message's first output byte (inflate_stream.ipp:
+// 475-496 with an empty window).
 __device__ __forceinline__ LaneRes decode_store(WaveLds& L, uint32_t wb, uint32_t start, uint32_t end,
                                                 uint32_t total_bits, const Tables& T, uint32_t P, uint32_t abs0,
-                                                uint32_t round0, uint32_t cap, bool raw, const WinRule& wr)
+                                                uint32_t round0, uint32_t cap, bool raw)
 {
     LaneRes r;
     r.n = 0;
@@ -364,7 +347,7 @@ __device__ __forceinline__ LaneRes decode_store(WaveLds& L, uint32_t wb, uint32_
         const uint32_t abs = abs0 + r.bytes;
         if (raw && abs >= cap) { r.ev = EV_FULL; break; }
         if (t.olen > 1 || (t.info >> 16)) {
-            if (dist_bad<RS>(t.info & 0xffffu, abs, t.olen, cap, wr)) { r.ev = EV_ERROR; r.err = ST_INVALID_DISTANCE; break; }
+            if ((t.info & 0xffffu) > abs) { r.ev = EV_ERROR; r.err = ST_INVALID_DISTANCE; break; }
         }
         if (abs >= cap) { r.ev = EV_FULL; break; }
         L.tok[P + r.n] = t.info;
@@ -458,12 +441,11 @@ __device__ __forceinline__ void expand_round(WaveLds& L, Out& o, uint32_t nbytes
         const uint32_t info = act ? L.tok[T] : 0u;
         const uint32_t len = info >> 16;
         uint32_t val = info & 0xffu;
-        // < 0: the window before the slot (a resumed per-stream decode)
         int32_t src = (int32_t)q - (int32_t)(info & 0xffffu);
         bool pend = false;
         if (act && len) {
             if (src >= (int32_t)c) pend = true;
-            else if (src >= 0 && (uint32_t)src + RING >= wend) val = L.ring[src & RING_MASK];
+            else if ((uint32_t)src + RING >= wend) val = L.ring[src & RING_MASK];
             else val = gbyte(o.g + src);
         }
         // matches reaching into this chunk: pointer jumping
@@ -488,53 +470,19 @@ __device__ __forceinline__ void expand_round(WaveLds& L, Out& o, uint32_t nbytes
 
 static __constant__ const uint8_t kClenOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
-// Per-stream resume (RS): start from rc.rin's checkpoint instead of a fresh
-// state, record the last token boundary reached in `ck` (written to rc.rout
-// by the caller), and follow the per-call window rule.
-struct Ckpt {
-    uint32_t bit, out, mode, last, srem;
-};
-
-template <bool RS>
-__device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t& out_len, int32_t& status,
-                            const bpmd_resume_call& rc)
+__device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t& out_len, int32_t& status)
 {
     const unsigned lane = lane_id();
     const uint32_t total_bits = m.total * 8;
     int32_t st = ST_OK;
     const int32_t full_status = raw ? ST_OK : ST_NEED_BUFFERS;
-    WinRule wr;
-    wr.hist = RS ? rc.hist : 0u;
-    wr.D = RS ? rc.D : 0u;
-    wr.cw = RS ? rc.cw : 0u;
-    Ckpt ck;
-    ck.bit = RS ? rc.rin->bit : 0u;
-    ck.out = 0;
-    ck.mode = RS ? rc.rin->mode : (uint32_t)BPMD_RM_TYPE;
-    ck.last = RS ? rc.rin->last : 0u;
-    ck.srem = RS ? rc.rin->srem : 0u;
-    uint32_t at_type = 0, at_hdr = 0, why = BPMD_RW_STARVED;
-    auto finish = [&](uint32_t end_bit) {
-        if (RS && lane == 0) {
-            rc.rout->bit = ck.bit;
-            rc.rout->out = ck.out;
-            rc.rout->mode = ck.mode;
-            rc.rout->last = ck.last;
-            rc.rout->srem = ck.srem;
-            rc.rout->end_bit = end_bit;
-            rc.rout->at_type = at_type;
-            rc.rout->at_hdr = at_hdr;
-            rc.rout->why = why;
-        }
-    };
     if (m.total == 0) {   // raw mode, no input: no progress (inflate_stream.ipp:113-117)
         out_len = 0;
         status = ST_NEED_BUFFERS;
-        finish(ck.bit);
         return;
     }
     PROF_DECL;
-    uint32_t wbase = RS ? (ck.bit >> 3) & ~3u : 0u;   // window start, bytes (multiple of 4)
+    uint32_t wbase = 0;   // window start, bytes (multiple of 4)
     load_window<WIN_WORDS>(L.win, m, wbase);
     wave_sync();
     PROF_LAP(10);
@@ -552,40 +500,21 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
     };
     auto ubits = [&](uint32_t p, unsigned n) -> uint32_t { return lowbits(peek64(L.win, p - wbase * 8), n); };
 
-    uint32_t pos = ck.bit;   // stream bit position (wave-uniform)
-    bool last = ck.last != 0;
+    uint32_t pos = 0;   // stream bit position (wave-uniform)
+    bool last = false;
     uint32_t est16 = 8 * 16;   // estimated bits per token, x16
-    // a resumed call enters the block its checkpoint is in; Flush::block and
-    // Flush::trees stop at the next block boundary (inflate_stream.ipp:127-141),
-    // except the one a call starting in TYPE mode begins at
-    uint32_t resume = ck.mode;
-    bool first = true;
 
     for (;;) {
-        const uint32_t rm = resume;
-        resume = BPMD_RM_TYPE;
         unsigned type;
-        if (rm == BPMD_RM_TYPE) {
+        {
             // ---- TYPEDO (inflate_stream.ipp:146-182)
-            if (RS) {
-                ck.bit = pos;
-                ck.out = o.pos;
-                ck.mode = BPMD_RM_TYPE;
-                ck.last = last;
-                if (rc.flush != BPMD_RF_SYNC && !first) { at_type = 1; why = BPMD_RW_FLUSH; break; }
-            }
-            first = false;
-            if (last) { st = ST_END_OF_STREAM; why = BPMD_RW_END; break; }
+            if (last) { st = ST_END_OF_STREAM; break; }
             ensure(pos, 700);
-            if (total_bits - pos < 3) { at_type = 1; break; }
+            if (total_bits - pos < 3) break;
             const uint32_t hdr = ubits(pos, 3);
             pos += 3;
             last = (hdr & 1) != 0;
             type = hdr >> 1;
-        } else {
-            first = false;
-            type = rm == BPMD_RM_STORED ? 0u : rm == BPMD_RM_FIXED ? 1u : 2u;
-            ensure(pos, 700);
         }
         Tables T;
         T.ltab = L.tab;
@@ -595,27 +524,12 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
 
         if (type == 0) {
             // ---- STORED / COPY (ipp:184-220)
-            uint32_t v;
-            if (rm == BPMD_RM_TYPE) {
-                pos = (pos + 7) & ~7u;
-                if (pos > total_bits || total_bits - pos < 32) break;
-                v = ubits(pos, 16);
-                const uint32_t nv = ubits(pos + 16, 16);
-                if (v != (nv ^ 0xffffu)) { st = ST_INVALID_STORED_LENGTH; break; }
-                pos += 32;
-                if (RS && rc.flush == BPMD_RF_TREES) {   // COPY_: Flush::trees returns here
-                    ck.bit = pos;
-                    ck.out = o.pos;
-                    ck.mode = BPMD_RM_STORED;
-                    ck.last = last;
-                    ck.srem = v;
-                    at_hdr = 1;
-                    why = BPMD_RW_FLUSH;
-                    break;
-                }
-            } else {
-                v = ck.srem;
-            }
+            pos = (pos + 7) & ~7u;
+            if (pos > total_bits || total_bits - pos < 32) break;
+            const uint32_t v = ubits(pos, 16);
+            const uint32_t nv = ubits(pos + 16, 16);
+            if (v != (nv ^ 0xffffu)) { st = ST_INVALID_STORED_LENGTH; break; }
+            pos += 32;
             const uint32_t from = pos >> 3;
             const uint32_t have = m.total - from;
             uint32_t n = v < have ? v : have;
@@ -631,52 +545,13 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
                 done += piece;
             }
             pos += n * 8;
-            if (RS && n < v) {   // still inside the block
-                ck.bit = pos;
-                ck.out = o.pos;
-                ck.mode = BPMD_RM_STORED;
-                ck.last = last;
-                ck.srem = v - n;
-            }
-            if (full) { st = full_status; why = BPMD_RW_FULL; break; }
+            if (full) { st = full_status; break; }
             if (n < v) break;   // input ends inside the block
             continue;
         } else if (type == 1) {
             for (unsigned k = lane; k < 512; k += WAVE) L.tab[k] = g_fixed_lens[k];
             if (lane < 32) L.tab[512 + lane] = g_fixed_dists[lane];
             wave_sync();
-            if (RS && rm == BPMD_RM_TYPE && rc.flush == BPMD_RF_TREES) {   // LEN_ (ipp:164-168)
-                ck.bit = pos;
-                ck.out = o.pos;
-                ck.mode = BPMD_RM_FIXED;
-                ck.last = last;
-                at_hdr = 1;
-                why = BPMD_RW_FLUSH;
-                break;
-            }
-        } else if (type == 2 && RS && rm == BPMD_RM_DYN) {
-            // resumed inside a dynamic block: rebuild its tables from the
-            // code lengths the checkpoint carries
-            const unsigned nlen = rc.rin->nlen, ndist = rc.rin->ndist;
-            for (unsigned i = lane; i < nlen + ndist; i += WAVE) {
-                L.u.h.lens[i] = rc.rin->lens[i];
-                rc.rout->lens[i] = rc.rin->lens[i];
-            }
-            if (lane == 0) {
-                rc.rout->nlen = nlen;
-                rc.rout->ndist = ndist;
-            }
-            wave_sync();
-            unsigned lroot = 0, lused = 0, lmin = 0, droot = 0, dused = 0, dmin = 0;
-            int r = build_table_wave<BUILD_LENS>(L.u.h.lens, nlen, L.tab, 9, L.u.h.ts, lroot, lused, lmin);
-            wave_sync();
-            if (!r) r = build_table_wave<BUILD_DISTS>(L.u.h.lens + nlen, ndist, L.tab + lused, 6, L.u.h.ts, droot,
-                                                      dused, dmin);
-            wave_sync();
-            if (r) { st = r; break; }   // cannot happen: the tables were built from these lengths before
-            T.lroot = lroot;
-            T.droot = droot;
-            T.dtab = L.tab + lused;
         } else if (type == 2) {
             // ---- TABLE / LENLENS / CODELENS (ipp:222-354)
             if (total_bits - pos < 14) break;
@@ -834,24 +709,6 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
             T.lroot = lroot;
             T.droot = droot;
             T.dtab = L.tab + lused;
-            if (RS) {
-                // the checkpoints inside this block carry its code lengths
-                // (the round bitmap overwrites them in LDS)
-                for (unsigned i = lane; i < nlen + ndist; i += WAVE) rc.rout->lens[i] = L.u.h.lens[i];
-                if (lane == 0) {
-                    rc.rout->nlen = nlen;
-                    rc.rout->ndist = ndist;
-                }
-                if (rc.flush == BPMD_RF_TREES) {   // LEN_ (ipp:350-352)
-                    ck.bit = pos;
-                    ck.out = o.pos;
-                    ck.mode = BPMD_RM_DYN;
-                    ck.last = last;
-                    at_hdr = 1;
-                    why = BPMD_RW_FLUSH;
-                    break;
-                }
-            }
         } else {
             st = ST_INVALID_BLOCK_TYPE;
             break;
@@ -865,12 +722,6 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
         while (!stop && !block_end) {
             PROF_CNT(6, 1);
             const uint32_t S = pos;
-            if (RS) {   // a round starts at a token boundary
-                ck.bit = S;
-                ck.out = o.pos;
-                ck.mode = type == 1 ? BPMD_RM_FIXED : BPMD_RM_DYN;
-                ck.last = last;
-            }
             const uint32_t rem = total_bits > S ? total_bits - S : 0;
             // segments keep ~SEG_TOKENS tokens even when the block is short:
             // shorter ones would rarely re-synchronise; lanes past the end of
@@ -957,7 +808,7 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
             c.err = 0;
             c.trips = 0;
             if (lane <= k)
-                c = decode_store<RS>(L, wb, start, seg1, total_bits, T, P, o.pos + O, o.pos, o.cap, raw, wr);
+                c = decode_store(L, wb, start, seg1, total_bits, T, P, o.pos + O, o.pos, o.cap, raw);
             wave_sync();
             const uint64_t evm2 = __ballot(lane <= k && c.ev != EV_NONE);
             const unsigned ke = first_lane(evm2);
@@ -984,7 +835,6 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
                 break;
             case EV_ERROR:
                 st = (int32_t)kerr;
-                why = BPMD_RW_END;
                 stop = true;
                 break;
             case EV_STARVED:
@@ -994,7 +844,6 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
             default:   // EV_FULL / EV_PARTIAL
                 st = full_status;
                 pos = kexit;
-                why = BPMD_RW_FULL;
                 stop = true;
                 break;
             }
@@ -1006,19 +855,16 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
     ring_flush(L, o, o.flushed, o.pos);
     PROF_LAP(12);
     PROF_FLUSH();
-    finish(pos);
     out_len = o.pos;
     status = st;
 }
 
-template <bool RS>
 __global__ void __launch_bounds__(WAVE)
 inflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                const uint32_t* __restrict__ in_len, uint32_t n_msgs, uint8_t* __restrict__ out,
                const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
                uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t raw,
-               const uint32_t* __restrict__ mask_key, uint32_t min_in, bpmd_resume_call rc,
-               uint32_t* __restrict__ qctr)
+               const uint32_t* __restrict__ mask_key, uint32_t min_in, uint32_t* __restrict__ qctr)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     WaveLds& L = *reinterpret_cast<WaveLds*>(smem);
@@ -1035,7 +881,7 @@ inflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
         o.flushed = 0;
         uint32_t ol = 0;
         int32_t st = 0;
-        inflate_msg<RS>(L, m, o, raw != 0, ol, st, rc);
+        inflate_msg(L, m, o, raw != 0, ol, st);
         if (lane_id() == 0) {
             out_len[msg] = ol;
             status[msg] = st;
@@ -1100,21 +946,8 @@ extern "C" int bpmd_internal_inflate_keyed_split(const uint8_t* in, const uint64
         qctr = (uint32_t*)bpmd_internal_scratch(stream, 256, 6);
         if (!qctr || hipMemsetAsync(qctr, 0, sizeof(uint32_t), stream) != hipSuccess) return (int)hipErrorOutOfMemory;
     }
-    hipLaunchKernelGGL(inflate_kernel<false>, dim3(grid), dim3(WAVE), lds, stream, in, in_off, in_len, n, out,
-                       out_off, out_cap, out_len, status, raw, mask_key, min_in, bpmd_resume_call{}, qctr);
-    return (int)hipGetLastError();
-}
-
-// One per-stream write() (pmd_stream.hip): a single raw-mode message resumed
-// at rc.rin's checkpoint; the output slot is preceded by rc.hist window bytes.
-extern "C" int bpmd_internal_inflate_resume(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
-                                            uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
-                                            uint32_t* out_len, int32_t* status, bpmd_resume_call rc,
-                                            hipStream_t stream)
-{
-    using namespace bpmd;
-    hipLaunchKernelGGL(inflate_kernel<true>, dim3(1), dim3(WAVE), sizeof(WaveLds), stream, in, in_off, in_len, 1u,
-                       out, out_off, out_cap, out_len, status, 1u, nullptr, 0u, rc, (uint32_t*)nullptr);
+    hipLaunchKernelGGL(inflate_kernel, dim3(grid), dim3(WAVE), lds, stream, in, in_off, in_len, n, out, out_off,
+                       out_cap, out_len, status, raw, mask_key, min_in, qctr);
     return (int)hipGetLastError();
 }
 

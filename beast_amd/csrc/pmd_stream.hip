@@ -1,7 +1,7 @@
 // pmd_stream.hip -- per-stream entry points behind the C++ compatibility
 // facade (include/beast_amd/zlib.hpp, include/boost/beast/zlib/*.hpp):
 // zlib::deflate_stream / zlib::inflate_stream write() semantics, executed by
-// the GPU kernels (a batch of one).  Host code only.
+// the GPU kernels.  Host code only.
 //
 // deflate: input is buffered until a flush; each flush compresses the
 //   buffered bytes on the GPU (blocks with BFINAL = 0, exact bit length
@@ -12,20 +12,14 @@
 //   00 00 FF FF, finish adds a final empty block and reports end_of_stream.
 //   Pending output, duplicate-flush need_buffers, stream_error and
 //   invalid_argument follow doWrite.
-// inflate: a resumable decoder (inflate_resume.h).  Each write() appends its
-//   input to the bytes kept since the last checkpoint, resumes the wave
-//   kernel there with the window (the last 2^windowBits output bytes before
-//   the checkpoint) in front of the output slot, hands out the bytes past
-//   those already delivered, then drops the input before the new checkpoint
-//   and slides the window on the device.  Per call the GPU decodes the new
-//   input plus at most one round again, and the stream holds O(window +
-//   one round + the caller's buffers) whatever the connection's age.  The
-//   reference's per-call rules are kept: the window check of a distance
-//   depends on the call boundaries (bpmd_resume_call), BAD mode answers
-//   need_buffers, DONE answers end_of_stream, Flush::block / Flush::trees stop
-//   at block boundaries / after a block header.  Input is reported consumed
-//   whole (the reference can leave input unconsumed when avail_out runs out
-//   first; here those bytes are kept and decoded by later calls).
+// inflate: the reference's decoder state lives on the device (zstream.h) and
+//   each write() is one launch of the per-stream kernel (pmd_zstream.hip),
+//   which runs inflate_stream.ipp's state machine with its bit reservoir and
+//   window: the call uploads the caller's input, the kernel decodes exactly
+//   what the reference would, and the host copies the output back and
+//   advances z_params by the kernel's done() record -- the reference's
+//   total_in (input left unconsumed stays with the caller), total_out and
+//   data_type; an error returns without advancing them, as err() does.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -34,12 +28,11 @@
 #include <vector>
 
 #include "../../include/beast_pmd.h"
-#include "inflate_resume.h"
+#include "zstream.h"
 
-extern "C" int bpmd_internal_inflate_resume(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
-                                            uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
-                                            uint32_t* out_len, int32_t* status, bpmd_resume_call rc,
-                                            hipStream_t stream);
+extern "C" int bpmd_internal_zstream_write(void* st, const uint8_t* in, uint64_t n_in, uint8_t* out, uint64_t cap,
+                                           int flush, void* res, hipStream_t stream);
+extern "C" void bpmd_internal_scratch_release(hipStream_t stream);
 extern "C" int bpmd_internal_deflate_bits(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                           uint32_t n, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                                           uint32_t* out_len, int32_t* status, uint32_t* out_bits, int level,
@@ -49,20 +42,15 @@ struct bpmd_stream {
     bool is_deflate = true;
     // deflate parameters
     int level = 6, wbits = 15, mem_level = 9, strategy = 0;
-    // inflate parameters and decoder state (inflate_resume.h)
+    // inflate: windowBits, device state (zstream.h State + Result), call buffers
     int inf_wbits = 15;
-    int inf_mode = 0;           // 0 decoding, 1 DONE (end_of_stream), 2 BAD
-    bpmd_resume ck{};           // checkpoint; ck.bit counts from in[0]
-    uint32_t hist = 0;          // window bytes = min(output before the checkpoint, 2^wbits)
-    uint64_t in_abs = 0;        // stream offset of in[0]
-    uint64_t ref_pos = 0;       // input bytes the reference would have consumed so far
-    uint32_t wcur = 0;          // which device window/output buffer holds the window
-    uint8_t* dwo[2] = {nullptr, nullptr};   // [2^15 window][output slot] each
-    size_t dwo_cap = 0;         // output slot bytes of each
-    uint8_t* dctl = nullptr;    // meta + checkpoint in/out
-    uint8_t* din = nullptr;     // pending input
+    void* zst = nullptr;
+    bool zreset = true;         // a reset() to apply before the next write()
+    uint8_t* din = nullptr;
     size_t din_cap = 0;
-    // buffered input (deflate: message bytes; inflate: compressed bytes since the checkpoint)
+    uint8_t* dout = nullptr;
+    size_t dout_cap = 0;
+    // deflate: buffered message bytes
     std::vector<uint8_t> in;
     // deflate: output not yet handed out, plus < 8 pending bits
     std::vector<uint8_t> pend;
@@ -74,8 +62,6 @@ struct bpmd_stream {
     bool inited = false;        // inited_ (deflate_stream.hpp:252): set by the first write after a reset
     bool tuned = false;         // tune() values in force (until reset / a level change)
     int tune4[4] = {0, 0, 0, 0};
-    // inflate: bytes decoded past the checkpoint and already handed out
-    size_t delivered = 0;
     // device scratch
     hipStream_t hs = nullptr;
     uint8_t* dmem = nullptr;
@@ -375,65 +361,55 @@ extern "C" int bpmd_inflate_stream_create(int window_bits, bpmd_stream** out)
 
 namespace {
 
-constexpr size_t kWinMax = size_t(1) << 15;   // window area in front of each output slot
-constexpr size_t kCtlMeta = 0, kCtlIn = 512, kCtlOut = 1024, kCtlBytes = 2048;
+using bpmd::zst::Head;
+using bpmd::zst::Result;
+using bpmd::zst::State;
 
-void reset_inflate(bpmd_stream* s, int window_bits)
+// inflate_stream::doReset (inflate_stream.ipp:55-72): HEAD, empty reservoir,
+// empty window of 2^windowBits
+Head fresh_head(int window_bits)
 {
-    // inflate_stream::reset (inflate_stream.ipp:55-72): fresh state, empty window
-    s->inf_wbits = window_bits;
-    s->inf_mode = 0;
-    s->ck = bpmd_resume{};
-    s->hist = 0;
-    s->in_abs = 0;
-    s->ref_pos = 0;
-    s->delivered = 0;
-    s->in.clear();
-    s->in.shrink_to_fit();
+    Head h{};
+    h.mode = bpmd::zst::HEAD;
+    h.wbits = (uint32_t)window_bits;
+    return h;
 }
 
-// device buffers for one call: pending input of n bytes, output slot of cap
-int ensure_inflate_device(bpmd_stream* s, size_t n, size_t cap)
+// the stream's device state, its result record and call buffers
+int ensure_zstate(bpmd_stream* s, size_t n_in, size_t cap)
 {
     if (!s->hs && hipStreamCreateWithFlags(&s->hs, hipStreamNonBlocking) != hipSuccess) return BPMD_R_HIP_ERROR;
-    if (!s->dctl && hipMalloc(&s->dctl, kCtlBytes) != hipSuccess) return BPMD_R_HIP_ERROR;
-    if (n > s->din_cap) {
+    if (!s->zst) {
+        if (hipMalloc(&s->zst, sizeof(State) + sizeof(Result)) != hipSuccess) {
+            s->zst = nullptr;
+            return BPMD_R_HIP_ERROR;
+        }
+        s->zreset = true;
+    }
+    if (s->zreset) {
+        const Head h = fresh_head(s->inf_wbits);
+        if (hipMemcpy(s->zst, &h, sizeof h, hipMemcpyHostToDevice) != hipSuccess) return BPMD_R_HIP_ERROR;
+        s->zreset = false;
+    }
+    // input and output buffers, with slack for the 16-byte input staging loads
+    if (n_in + 64 > s->din_cap) {
         if (s->din) (void)hipFree(s->din);
         s->din = nullptr;
         s->din_cap = 0;
-        const size_t c = std::max<size_t>(n + n / 2, 4096);
-        if (hipMalloc(&s->din, c + 64) != hipSuccess) return BPMD_R_HIP_ERROR;
+        const size_t c = std::max<size_t>(n_in + n_in / 2 + 64, 4096);
+        if (hipMalloc(&s->din, c) != hipSuccess) return BPMD_R_HIP_ERROR;
         s->din_cap = c;
     }
-    if (cap > s->dwo_cap || !s->dwo[0]) {
-        // grow both; the window moves to the new current buffer
-        const size_t c = std::max<size_t>(cap + cap / 2, 1 << 16);
-        uint8_t* nb[2] = {nullptr, nullptr};
-        for (int k = 0; k < 2; ++k)
-            if (hipMalloc(&nb[k], kWinMax + c + 64) != hipSuccess) {
-                if (nb[0]) (void)hipFree(nb[0]);
-                return BPMD_R_HIP_ERROR;
-            }
-        if (s->hist && s->dwo[s->wcur] &&
-            hipMemcpyAsync(nb[0] + kWinMax - s->hist, s->dwo[s->wcur] + kWinMax - s->hist, s->hist,
-                           hipMemcpyDeviceToDevice, s->hs) != hipSuccess)
-            return BPMD_R_HIP_ERROR;
-        if (hipStreamSynchronize(s->hs) != hipSuccess) return BPMD_R_HIP_ERROR;
-        for (int k = 0; k < 2; ++k)
-            if (s->dwo[k]) (void)hipFree(s->dwo[k]);
-        s->dwo[0] = nb[0];
-        s->dwo[1] = nb[1];
-        s->wcur = 0;
-        s->dwo_cap = c;
+    if (cap + 64 > s->dout_cap) {
+        if (s->dout) (void)hipFree(s->dout);
+        s->dout = nullptr;
+        s->dout_cap = 0;
+        const size_t c = std::max<size_t>(cap + cap / 2 + 64, 4096);
+        if (hipMalloc(&s->dout, c) != hipSuccess) return BPMD_R_HIP_ERROR;
+        s->dout_cap = c;
     }
     return BPMD_R_OK;
 }
-
-struct InfMeta {
-    uint64_t in_off, out_off;
-    uint32_t in_len, out_cap, out_len;
-    int32_t status;
-};
 
 }  // namespace
 
@@ -441,7 +417,8 @@ extern "C" int bpmd_inflate_stream_reset(bpmd_stream* s, int window_bits)
 {
     if (!s || s->is_deflate) return BPMD_R_INVALID_ARGUMENT;
     if (window_bits < 8 || window_bits > 15) return BPMD_R_DOMAIN_ERROR;
-    reset_inflate(s, window_bits);
+    s->inf_wbits = window_bits;
+    s->zreset = true;   // applied before the next write()
     return BPMD_R_OK;
 }
 
@@ -457,156 +434,59 @@ extern "C" int bpmd_inflate_stream_write(bpmd_stream* s, bpmd_zparams* zs, int f
     if (!s || s->is_deflate || !zs || flush < BPMD_FLUSH_NONE || flush > BPMD_FLUSH_TREES)
         return BPMD_R_INVALID_ARGUMENT;
     if ((!zs->next_in && zs->avail_in) || (!zs->next_out && zs->avail_out)) return BPMD_STREAM_ERROR;
-    zs->data_type = 2;   // unknown until a call decodes
-    // DONE: end_of_stream without touching the buffers; BAD: no progress
-    // (inflate_stream.ipp:516-529, done() at :88-119)
-    if (s->inf_mode == 1) return BPMD_END_OF_STREAM;
-    if (s->inf_mode == 2) return BPMD_NEED_BUFFERS;
     int r = bpmd_init();
     if (r) return r;
-    const size_t n_in = zs->avail_in;
-    const size_t kept = s->in.size();
-    if (n_in) {
-        const uint8_t* p = (const uint8_t*)zs->next_in;
-        s->in.insert(s->in.end(), p, p + n_in);
+    const size_t n = zs->avail_in;
+    // Output room handed to the kernel.  A call cannot produce more than the
+    // pending match (<= 258) plus 258 bytes per 2 bits of the input and the
+    // reservoir (<= 32 bits), so a room of at least that plus 258 leaves the
+    // reference's "avail_out >= 258" fast-path test unchanged.
+    const size_t bound = 1040 * n + 8192;
+    const size_t cap = std::min<size_t>(zs->avail_out, bound);
+    if ((r = ensure_zstate(s, n, cap)) != 0) return r;
+    const hipStream_t hs = s->hs;
+    Result res{};
+    void* dres = (uint8_t*)s->zst + sizeof(State);
+    bool ok = (n == 0 || hipMemcpyAsync(s->din, zs->next_in, n, hipMemcpyHostToDevice, hs) == hipSuccess) &&
+              bpmd_internal_zstream_write(s->zst, s->din, n, s->dout, cap, flush, dres, hs) == 0 &&
+              hipMemcpyAsync(&res, dres, sizeof res, hipMemcpyDeviceToHost, hs) == hipSuccess &&
+              hipStreamSynchronize(hs) == hipSuccess;
+    // the bytes are in the caller's buffer whether or not done() publishes them
+    ok = ok && (res.out_used == 0 ||
+                hipMemcpy(zs->next_out, s->dout, res.out_used, hipMemcpyDeviceToHost) == hipSuccess);
+    if (!ok) return BPMD_R_HIP_ERROR;   // the device state is unchanged only if the kernel never ran
+    if (res.published) {
+        zs->next_in = (const uint8_t*)zs->next_in + res.in_used;
+        zs->avail_in -= res.in_used;
+        zs->total_in += res.in_used;
+        zs->next_out = (uint8_t*)zs->next_out + res.out_used;
+        zs->avail_out -= res.out_used;
+        zs->total_out += res.out_used;
+        zs->data_type = res.data_type;
     }
-    const size_t n = s->in.size();
-    const uint32_t W = 1u << s->inf_wbits;
-    // output slot: what is re-decoded (delivered) plus this call's room, which
-    // the pending input could not exceed anyway (<= 258 bytes per 2 bits)
-    const size_t room = std::min<size_t>(zs->avail_out, 1040 * n + 1024);
-    const size_t cap = s->delivered + room;
-    if (n > 0xFFFFFFF0u || cap > 0xFFFFFFF0u) {
-        s->in.resize(kept);
-        return BPMD_R_INVALID_ARGUMENT;
-    }
-    size_t fresh = 0;
-    int32_t st = BPMD_OK;
-    bpmd_resume out_ck{};
-    const uint64_t ref_before = s->ref_pos;
-    if (n == 0) {
-        st = BPMD_NEED_BUFFERS;   // nothing to decode (raw mode, no input)
-        out_ck = s->ck;
-    } else {
-        if ((r = ensure_inflate_device(s, n, cap)) != 0) {
-            s->in.resize(kept);
-            return r;
-        }
-        uint8_t* wo = s->dwo[s->wcur];
-        InfMeta m{};
-        m.in_off = 0;
-        m.out_off = kWinMax;
-        m.in_len = (uint32_t)n;
-        m.out_cap = (uint32_t)cap;
-        const hipStream_t hs = s->hs;
-        bool ok = hipMemcpyAsync(s->dctl + kCtlMeta, &m, sizeof m, hipMemcpyHostToDevice, hs) == hipSuccess &&
-                  hipMemcpyAsync(s->dctl + kCtlIn, &s->ck, sizeof s->ck, hipMemcpyHostToDevice, hs) == hipSuccess &&
-                  hipMemcpyAsync(s->din, s->in.data(), n, hipMemcpyHostToDevice, hs) == hipSuccess;
-        bpmd_resume_call rc;
-        rc.rin = (const bpmd_resume*)(s->dctl + kCtlIn);
-        rc.rout = (bpmd_resume*)(s->dctl + kCtlOut);
-        rc.hist = s->hist;
-        rc.D = (uint32_t)s->delivered;
-        rc.cw = (uint32_t)std::min<size_t>(s->hist + s->delivered, W);
-        rc.flush = flush == BPMD_FLUSH_BLOCK ? BPMD_RF_BLOCK : flush == BPMD_FLUSH_TREES ? BPMD_RF_TREES
-                                                                                         : BPMD_RF_SYNC;
-        InfMeta* dm = (InfMeta*)(s->dctl + kCtlMeta);
-        ok = ok && bpmd_internal_inflate_resume(s->din, &dm->in_off, &dm->in_len, wo, &dm->out_off, &dm->out_cap,
-                                                &dm->out_len, &dm->status, rc, hs) == 0;
-        ok = ok && hipMemcpyAsync(&m, s->dctl + kCtlMeta, sizeof m, hipMemcpyDeviceToHost, hs) == hipSuccess &&
-             hipMemcpyAsync(&out_ck, s->dctl + kCtlOut, sizeof out_ck, hipMemcpyDeviceToHost, hs) == hipSuccess &&
-             hipStreamSynchronize(hs) == hipSuccess;
-        if (!ok) {
-            s->in.resize(kept);
-            return BPMD_R_HIP_ERROR;
-        }
-        st = m.status;
-        fresh = m.out_len > s->delivered ? m.out_len - s->delivered : 0;
-        if (fresh && hipMemcpy(zs->next_out, wo + kWinMax + s->delivered, fresh, hipMemcpyDeviceToHost) != hipSuccess)
-            return BPMD_R_HIP_ERROR;
-        // advance the checkpoint: window <- the last W bytes before it
-        const uint32_t K = out_ck.out;
-        const uint32_t nh = (uint32_t)std::min<size_t>((size_t)s->hist + K, W);
-        if (K && st < BPMD_END_OF_STREAM) {
-            uint8_t* nw = s->dwo[s->wcur ^ 1];
-            if (hipMemcpyAsync(nw + kWinMax - nh, wo + kWinMax + K - nh, nh, hipMemcpyDeviceToDevice, hs) !=
-                hipSuccess)
-                return BPMD_R_HIP_ERROR;
-            s->wcur ^= 1;
-        }
-        const size_t used_bytes = out_ck.bit >> 3;
-        if (st == BPMD_END_OF_STREAM) {
-            // consumed up to the byte holding the last bit of the final block
-            const size_t end = (out_ck.bit + 7) >> 3;
-            const size_t take = end > kept ? std::min(end - kept, n_in) : 0;
-            zs->next_in = (const uint8_t*)zs->next_in + take;
-            zs->avail_in -= take;
-            zs->total_in += take;
-            zs->next_out = (uint8_t*)zs->next_out + fresh;
-            zs->avail_out -= fresh;
-            zs->total_out += fresh;
-            s->inf_mode = 1;
-            s->in.clear();
-            s->in.shrink_to_fit();
-            return BPMD_END_OF_STREAM;
-        }
-        if (st > BPMD_END_OF_STREAM) {
-            // a data error: the reference's err() returns without done(), so
-            // the bytes are in the caller's buffer but zs is not advanced
-            // (inflate_stream.ipp:121-125); the stream is BAD from now on
-            s->inf_mode = 2;
-            s->in.clear();
-            s->in.shrink_to_fit();
-            return st;
-        }
-        // the reference's consumption: an exhausted input is taken whole; a
-        // call that stopped early (Flush::block / trees, a full output)
-        // leaves the bytes past where it stopped (bits held < 8 after
-        // inflate_fast's rewind, inflate_stream.ipp:1101-1112)
-        const uint64_t stop_at = s->in_abs + ((out_ck.end_bit + 7) >> 3);
-        if (out_ck.why == BPMD_RW_STARVED) s->ref_pos = s->in_abs + n;
-        else if (stop_at > s->ref_pos) s->ref_pos = std::min<uint64_t>(stop_at, s->in_abs + n);
-        s->hist = nh;
-        s->delivered = s->delivered + fresh - K;
-        s->in.erase(s->in.begin(), s->in.begin() + (ptrdiff_t)used_bytes);
-        s->in_abs += used_bytes;
-        out_ck.bit -= (uint32_t)(8 * used_bytes);
-        // data_type (inflate_stream.ipp:108-112): bits held, last block, block boundary, after a header
-        const uint32_t held = out_ck.end_bit >= 8 * used_bytes ? (uint32_t)(8 * n - out_ck.end_bit) : 0u;
-        zs->data_type = (int)((held < 64 ? held : 0u) + (out_ck.last ? 64u : 0u) + (out_ck.at_type ? 128u : 0u) +
-                              (out_ck.at_hdr ? 256u : 0u));
-        s->ck = out_ck;
-        if (s->in.capacity() > 4 * s->in.size() + 65536) s->in.shrink_to_fit();
-    }
-    zs->next_in = (const uint8_t*)zs->next_in + n_in;
-    zs->avail_in = 0;
-    zs->total_in += n_in;
-    zs->next_out = (uint8_t*)zs->next_out + fresh;
-    zs->avail_out -= fresh;
-    zs->total_out += fresh;
-    // done(): no progress -- nothing the reference would have consumed, nothing produced
-    if ((s->ref_pos == ref_before && fresh == 0) || flush == BPMD_FLUSH_FINISH) return BPMD_NEED_BUFFERS;
-    return BPMD_OK;
+    return res.ec;
 }
 
 extern "C" int bpmd_inflate_stream_footprint(const bpmd_stream* s, size_t* host_bytes, size_t* device_bytes)
 {
     if (!s || s->is_deflate) return BPMD_R_INVALID_ARGUMENT;
-    if (host_bytes) *host_bytes = s->in.capacity();
+    if (host_bytes) *host_bytes = 0;   // the reservoir and window live on the device
     if (device_bytes)
-        *device_bytes = (s->dctl ? kCtlBytes : 0) + (s->din ? s->din_cap + 64 : 0) +
-                        (s->dwo[0] ? 2 * (kWinMax + s->dwo_cap + 64) : 0);
+        *device_bytes = (s->zst ? sizeof(State) + sizeof(Result) : 0) + s->din_cap + s->dout_cap;
     return BPMD_R_OK;
 }
 
 extern "C" void bpmd_stream_destroy(bpmd_stream* s)
 {
     if (!s) return;
+    if (s->hs) (void)hipStreamSynchronize(s->hs);
     if (s->dmem) (void)hipFree(s->dmem);
-    if (s->dctl) (void)hipFree(s->dctl);
+    if (s->zst) (void)hipFree(s->zst);
     if (s->din) (void)hipFree(s->din);
-    for (int k = 0; k < 2; ++k)
-        if (s->dwo[k]) (void)hipFree(s->dwo[k]);
-    if (s->hs) (void)hipStreamDestroy(s->hs);
+    if (s->dout) (void)hipFree(s->dout);
+    if (s->hs) {
+        bpmd_internal_scratch_release(s->hs);
+        (void)hipStreamDestroy(s->hs);
+    }
     delete s;
 }

@@ -1,0 +1,615 @@
+// pmd_zstream.hip -- the per-stream inflater behind zlib::inflate_stream
+// (include/boost/beast/zlib/inflate_stream.hpp:63-213): one write() per
+// launch, on the GPU, with the reference's state carried on the device.
+//
+// Why a state machine and not the batch decoders.  Beast's inflate_stream
+// keeps everything between write() calls -- mode, the 32-bit bit reservoir,
+// a half-decoded symbol, the code tables, the 2^windowBits window
+// (inflate_stream.ipp:74-535, bitstream.hpp:49-194, window.hpp:51-144) --
+// and websocket::stream advances its read buffer by exactly the total_in a
+// call reports (read.hpp:1342-1343, impl_base.hpp:183-187).  How many bytes
+// a call consumes depends on that state: the slow path pulls bytes one at a
+// time until a lookup has the bits it asks for (root, or root + sub-table
+// bits), inflate_fast pulls 16 bits at a time and hands whole bytes back when
+// it returns (inflate_stream.ipp:1111-1112), and which of the two runs
+// depends on how much input and output room is left.  The batch kernels
+// decode whole messages and cannot reproduce that, so a per-stream call runs
+// the reference's decoder itself: the same modes, the same fills, drops and
+// rewinds, the same window rule, so next_in / avail_in / total_in / next_out
+// / avail_out / total_out / data_type and the zlib::error are the
+// reference's after every call, including calls that stop inside a symbol,
+// a header or a stored block, and errors (which return without done()).
+//
+// Execution: one wave.  The decoder's control flow is wave-uniform (values
+// read from LDS are made uniform with readfirstlane, so branches are scalar);
+// the lanes share the bulk work -- code tables (huff_wave.h, slot-for-slot
+// equal to inflate_table), match copies (64 bytes per step out of a 64 KiB
+// LDS history ring), stored-block copies, loading the window into the ring
+// the first time a distance reaches it, the window update, and the output
+// stores.  Input is staged through LDS 4 KiB at a time.
+// The decoder body (zstream_run) is plain wave-uniform C++; with
+// BPMD_ZSTREAM_HOST the same text compiles for the host with one-lane
+// meanings of the intrinsics (tests/model/zstream_host.py), so the CPU suite
+// checks it against the oracle too.
+#ifndef BPMD_ZSTREAM_HOST
+#include "pmd_common.h"
+#include "huff_table.h"
+#include "huff_wave.h"
+#include "wave_util.h"
+#endif
+#include "zstream.h"
+
+namespace bpmd {
+namespace zst {
+
+constexpr uint32_t HR = 65536, HM = HR - 1;   // history ring: window + this call's output
+constexpr uint32_t IST = 4096;               // input staging
+constexpr uint64_t FLUSH_AT = 16384;          // unflushed output kept below this (ring room)
+
+struct alignas(16) Lds {
+    uint8_t hist[HR];
+    uint8_t ist[IST];
+    uint16_t tab[kCodes];
+    uint8_t lens[kLens];
+    uint8_t flens[288];   // fixed-block code lengths (fixedTables, inflate_stream.ipp:865-930)
+    WaveTableScratch ts;
+};
+
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ bool is_link(uint32_t s) { return slot_kind(s) == K_SPECIAL && slot_val(s) != V_INVALID; }
+
+__constant__ static const uint8_t kOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+enum : int { F_BLOCK = 1, F_FINISH = 5, F_TREES = 6 };   // zlib::Flush values that change doWrite
+
+__device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __restrict__ in, uint64_t n_in,
+                            uint8_t* __restrict__ out, uint64_t cap, int flush, Result* __restrict__ res)
+{
+    const unsigned lane = lane_id();
+    Head h = st->h;
+    const uint32_t wcap = 1u << h.wbits;
+
+    // tables and code lengths the current mode still needs
+    if (h.mode >= CODELENS && h.mode <= LIT)
+        for (unsigned i = lane; i < kCodes; i += WAVE) L.tab[i] = st->codes[i];
+    if (h.mode == LENLENS || h.mode == CODELENS)
+        for (unsigned i = lane; i < kLens; i += WAVE) L.lens[i] = st->lens[i];
+    bool tab_dirty = false, lens_dirty = false;
+
+    // ---- input: bytes [ib0, ib1) of this call's input are staged in LDS
+    uint64_t ip = 0, ib0 = 0, ib1 = 0;
+    auto stage = [&](uint64_t at) {
+        wave_sync();
+        ib0 = at & ~(uint64_t)15;
+        ib1 = ib0 + IST < n_in ? ib0 + IST : n_in;
+        for (uint32_t k = lane * 16; k < IST; k += WAVE * 16)
+            if (ib0 + k < n_in) *(uint4*)(L.ist + k) = *(const uint4*)(in + ib0 + k);
+        wave_sync();
+    };
+    // bit reservoir, bitstream.hpp: v_ holds n_ bits, bytes enter at bit n_
+    uint32_t bv = h.bv, bn = h.bn;
+    auto pull = [&]() {
+        if (ip < ib0 || ip >= ib1) stage(ip);
+        const uint32_t b = uni(L.ist[ip - ib0]);
+        ++ip;
+        if (bn < 32) bv += b << bn;
+        bn += 8;
+    };
+    auto fill = [&](uint32_t k) -> bool {   // bitstream::fill
+        while (bn < k) {
+            if (ip == n_in) return false;
+            pull();
+        }
+        return true;
+    };
+    auto peek = [&](uint32_t k) -> uint32_t { return k >= 32 ? bv : (bv & ((1u << k) - 1u)); };
+    auto drop = [&](uint32_t k) {
+        bv = k >= 32 ? 0u : bv >> k;
+        bn -= k;
+    };
+    auto take = [&](uint32_t k) -> uint32_t {
+        const uint32_t r = peek(k);
+        drop(k);
+        return r;
+    };
+    auto rewind = [&]() {   // bitstream::rewind: whole bytes back to the input
+        ip -= bn >> 3;
+        bn &= 7;
+        bv &= (1u << bn) - 1u;
+    };
+
+    // ---- output: this call's bytes go to the ring and out to `out`
+    uint64_t op = 0, flushed = 0;
+    auto flush_out = [&]() {
+        wave_sync();
+        for (uint64_t p = flushed + lane; p < op; p += WAVE) out[p] = L.hist[(uint32_t)p & HM];
+        flushed = op;
+        wave_sync();
+    };
+    auto put = [&](uint32_t b) {
+        if (lane == 0) L.hist[(uint32_t)op & HM] = (uint8_t)b;
+        ++op;
+    };
+    bool winld = false;
+    auto load_window = [&]() {   // window byte k back sits at ring position -k
+        wave_sync();
+        for (uint32_t k = 1 + lane; k <= h.wsize; k += WAVE)
+            L.hist[(HR - k) & HM] = st->win[(h.wpos - k) & (wcap - 1)];
+        winld = true;
+        wave_sync();
+    };
+    // n bytes copied from `dist` back (window, then this call's output): the
+    // history is contiguous, so byte j is history[op - dist + j mod dist]
+    auto copy_back = [&](uint32_t dist, uint32_t n) {
+        if (dist > op && !winld) load_window();
+        wave_sync();
+        for (uint32_t j0 = 0; j0 < n; j0 += WAVE) {
+            const uint32_t j = j0 + lane;
+            if (j < n) {
+                const uint32_t k = dist >= n ? j : j % dist;
+                const uint8_t b = L.hist[(uint32_t)(op - dist + k) & HM];
+                L.hist[(uint32_t)(op + j) & HM] = b;
+            }
+        }
+        op += n;
+        wave_sync();
+    };
+    auto copy_in = [&](uint32_t n) {   // a stored block's bytes
+        for (uint32_t done = 0; done < n;) {
+            const uint32_t piece = n - done < 8192u ? n - done : 8192u;
+            wave_sync();
+            for (uint32_t j = lane; j < piece; j += WAVE) L.hist[(uint32_t)(op + j) & HM] = in[ip + j];
+            ip += piece;
+            op += piece;
+            done += piece;
+            wave_sync();
+            if (op - flushed >= FLUSH_AT) flush_out();
+        }
+    };
+    // code tables into LDS; returns 0 or the zlib::error of inflate_table
+    auto build = [&](int type, const uint8_t* lens, unsigned n, unsigned at, unsigned req, uint32_t& root,
+                     uint32_t& used) -> int {
+        wave_sync();
+        unsigned r = 0, u = 0, lmin = 0;
+        int e;
+        if (type == BUILD_CODES) e = build_table_wave<BUILD_CODES>(lens, n, L.tab + at, req, L.ts, r, u, lmin);
+        else if (type == BUILD_LENS) e = build_table_wave<BUILD_LENS>(lens, n, L.tab + at, req, L.ts, r, u, lmin);
+        else e = build_table_wave<BUILD_DISTS>(lens, n, L.tab + at, req, L.ts, r, u, lmin);
+        wave_sync();
+        tab_dirty = true;
+        root = uni(r);
+        used = uni(u);
+        return (int)uni((uint32_t)e);
+    };
+
+    // ---- inflate_fast (inflate_stream.ipp:979-1113); 0 or an error (mode BAD)
+    auto fast = [&]() -> int32_t {
+        const uint64_t in_last = n_in - 5, out_last = cap - 257;
+        const uint32_t lmask = (1u << h.lroot) - 1u, dmask = (1u << h.droot) - 1u;
+        int32_t err = 0;
+        do {
+            if (bn < 15) {
+                pull();
+                pull();
+            }
+            uint32_t s = uni(L.tab[bv & lmask]);
+            if (is_link(s)) {   // 2nd-level code: root bits, then the sub-table's index bits
+                drop(h.lroot);
+                s = uni(L.tab[slot_val(s) + (bv & ((1u << slot_bits(s)) - 1u))]);
+            }
+            drop(slot_bits(s));
+            const uint32_t kind = slot_kind(s), val = slot_val(s);
+            if (kind == K_VAL) {
+                put(val);
+            } else if (kind == K_LEN) {
+                uint32_t len = kLenBase[val];
+                const uint32_t x = kLenExtra[val];
+                if (x) {
+                    if (bn < x) pull();
+                    len += bv & ((1u << x) - 1u);
+                    drop(x);
+                }
+                if (bn < 15) {
+                    pull();
+                    pull();
+                }
+                uint32_t d = uni(L.tab[h.dtab + (bv & dmask)]);
+                if (is_link(d)) {
+                    drop(h.droot);
+                    d = uni(L.tab[h.dtab + slot_val(d) + (bv & ((1u << slot_bits(d)) - 1u))]);
+                }
+                drop(slot_bits(d));
+                if (slot_kind(d) != K_VAL) {
+                    err = ST_INVALID_DISTANCE_CODE;
+                    break;
+                }
+                uint32_t dist = kDistBase[slot_val(d)];
+                const uint32_t dx = kDistExtra[slot_val(d)];
+                if (bn < dx) {
+                    pull();
+                    if (bn < dx) pull();
+                }
+                dist += bv & ((1u << dx) - 1u);
+                drop(dx);
+                if (dist > op) {   // from the window
+                    const uint64_t back = dist - op;
+                    if (back > h.wsize) {
+                        err = ST_INVALID_DISTANCE;
+                        break;
+                    }
+                    const uint32_t n = len < back ? len : (uint32_t)back;
+                    copy_back(dist, n);
+                    len -= n;
+                }
+                if (len) copy_back(dist, len);   // from this call's output (room >= 258 here)
+            } else if (kind == K_EOB) {
+                h.mode = TYPE;
+                break;
+            } else {
+                err = ST_INVALID_LITERAL_LENGTH;
+                break;
+            }
+            if (op - flushed >= FLUSH_AT) flush_out();
+        } while (ip < in_last && op < out_last);
+        if (err) h.mode = BAD;
+        rewind();
+        return err;
+    };
+
+    int32_t ec = 0;
+    int32_t published = 0;
+    int32_t data_type = 0;
+
+    if (h.mode == TYPE) h.mode = TYPEDO;
+    for (;;) {
+        switch (h.mode) {
+        case HEAD:
+            h.mode = TYPEDO;
+            continue;
+        case TYPE:
+            if (flush == F_BLOCK || flush == F_TREES) goto done;
+            [[fallthrough]];
+        case TYPEDO: {
+            if (h.last) {
+                drop(bn % 8);
+                h.mode = CHECK;
+                continue;
+            }
+            if (!fill(3)) goto done;
+            h.last = take(1);
+            const uint32_t t = take(2);
+            if (t == 0) {
+                h.mode = STORED;
+            } else if (t == 1) {
+                for (unsigned i = lane; i < 288; i += WAVE) L.flens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8;
+                uint32_t root, used;
+                build(BUILD_LENS, L.flens, 288, 0, 9, root, used);
+                h.lroot = root;
+                for (unsigned i = lane; i < 32; i += WAVE) L.flens[i] = 5;
+                uint32_t droot, dused;
+                build(BUILD_DISTS, L.flens, 32, used, 5, droot, dused);
+                h.droot = droot;
+                h.dtab = used;
+                h.mode = LEN_;
+                if (flush == F_TREES) goto done;
+            } else if (t == 2) {
+                h.mode = TABLE;
+            } else {
+                ec = ST_INVALID_BLOCK_TYPE;
+                h.mode = BAD;
+                goto quiet;
+            }
+            continue;
+        }
+        case STORED: {
+            drop(bn % 8);
+            if (!fill(32)) goto done;
+            const uint32_t v = peek(32);
+            h.length = v & 0xffffu;
+            if (h.length != ((v >> 16) ^ 0xffffu)) {
+                ec = ST_INVALID_STORED_LENGTH;
+                h.mode = BAD;
+                goto quiet;
+            }
+            bv = 0;   // bitstream::flush
+            bn = 0;
+            h.mode = COPY_;
+            if (flush == F_TREES) goto done;
+        }
+            [[fallthrough]];
+        case COPY_:
+            h.mode = COPY;
+            [[fallthrough]];
+        case COPY: {
+            uint64_t n = h.length;
+            if (n == 0) {
+                h.mode = TYPE;
+                continue;
+            }
+            if (n > n_in - ip) n = n_in - ip;
+            if (n > cap - op) n = cap - op;
+            if (n == 0) goto done;
+            copy_in((uint32_t)n);
+            h.length -= (uint32_t)n;
+            continue;
+        }
+        case TABLE:
+            if (!fill(14)) goto done;
+            h.nlen = take(5) + 257;
+            h.ndist = take(5) + 1;
+            h.ncode = take(4) + 4;
+            if (h.nlen > 286 || h.ndist > 30) {
+                ec = ST_TOO_MANY_SYMBOLS;
+                h.mode = BAD;
+                goto quiet;
+            }
+            h.have = 0;
+            h.mode = LENLENS;
+            [[fallthrough]];
+        case LENLENS: {
+            while (h.have < h.ncode) {
+                if (!fill(3)) goto done;
+                const uint32_t v = take(3);
+                if (lane == 0) L.lens[kOrder[h.have]] = (uint8_t)v;
+                lens_dirty = true;
+                ++h.have;
+            }
+            while (h.have < 19) {
+                if (lane == 0) L.lens[kOrder[h.have]] = 0;
+                ++h.have;
+            }
+            lens_dirty = true;
+            uint32_t root, used;
+            const int e = build(BUILD_CODES, L.lens, 19, 0, 7, root, used);
+            if (e) {   // inflate_stream.ipp:255-261: BAD, then done() reports it
+                ec = e;
+                h.mode = BAD;
+                continue;
+            }
+            h.lroot = root;
+            h.have = 0;
+            h.mode = CODELENS;
+        }
+            [[fallthrough]];
+        case CODELENS: {
+            const uint32_t want = h.nlen + h.ndist;
+            while (h.have < want) {
+                if (!fill(h.lroot)) goto done;
+                const uint32_t s = uni(L.tab[peek(h.lroot)]);
+                const uint32_t cb = slot_bits(s);
+                // the empty code's slots are {op 64, bits 1, val 0} (ipp:574-584)
+                const uint32_t val = slot_kind(s) == K_SPECIAL ? 0u : slot_val(s);
+                if (val < 16) {
+                    drop(cb);
+                    if (lane == 0) L.lens[h.have] = (uint8_t)val;
+                    ++h.have;
+                    lens_dirty = true;
+                    continue;
+                }
+                uint32_t rep, fv;
+                if (val == 16) {
+                    if (!fill(cb + 2)) goto done;
+                    drop(cb);
+                    if (h.have == 0) {
+                        ec = ST_INVALID_BIT_LENGTH_REPEAT;
+                        h.mode = BAD;
+                        goto quiet;
+                    }
+                    rep = 3 + take(2);
+                    wave_sync();
+                    fv = uni(L.lens[h.have - 1]);
+                } else if (val == 17) {
+                    if (!fill(cb + 3)) goto done;
+                    drop(cb);
+                    rep = 3 + take(3);
+                    fv = 0;
+                } else {
+                    if (!fill(cb + 7)) goto done;
+                    drop(cb);
+                    rep = 11 + take(7);
+                    fv = 0;
+                }
+                if (h.have + rep > want) {
+                    ec = ST_INVALID_BIT_LENGTH_REPEAT;
+                    h.mode = BAD;
+                    goto quiet;
+                }
+                wave_sync();
+                for (uint32_t j = lane; j < rep; j += WAVE) L.lens[h.have + j] = (uint8_t)fv;
+                h.have += rep;
+                lens_dirty = true;
+            }
+            wave_sync();
+            if (uni(L.lens[256]) == 0) {
+                ec = ST_MISSING_EOB;
+                h.mode = BAD;
+                goto quiet;
+            }
+            uint32_t lroot, lused, droot, dused;
+            int e = build(BUILD_LENS, L.lens, h.nlen, 0, 9, lroot, lused);
+            if (!e) e = build(BUILD_DISTS, L.lens + h.nlen, h.ndist, lused, 6, droot, dused);
+            if (e) {   // inflate_stream.ipp:336-349: BAD and return, without done()
+                ec = e;
+                h.mode = BAD;
+                goto quiet;
+            }
+            h.lroot = lroot;
+            h.droot = droot;
+            h.dtab = lused;
+            h.mode = LEN_;
+            if (flush == F_TREES) goto done;
+        }
+            [[fallthrough]];
+        case LEN_:
+            h.mode = LEN;
+            [[fallthrough]];
+        case LEN: {
+            if (n_in - ip >= 6 && cap - op >= 258) {
+                const int32_t e = fast();
+                if (e) {
+                    ec = e;
+                    goto quiet;
+                }
+                continue;
+            }
+            if (!fill(h.lroot)) goto done;
+            uint32_t s = uni(L.tab[peek(h.lroot)]);
+            if (is_link(s)) {
+                const uint32_t w = h.lroot + slot_bits(s);
+                if (!fill(w)) goto done;
+                s = uni(L.tab[slot_val(s) + (peek(w) >> h.lroot)]);
+                drop(h.lroot + slot_bits(s));
+            } else {
+                drop(slot_bits(s));
+            }
+            const uint32_t kind = slot_kind(s), val = slot_val(s);
+            if (kind == K_VAL) {
+                h.length = val;
+                h.mode = LIT;
+                continue;
+            }
+            if (kind == K_EOB) {
+                h.mode = TYPE;
+                continue;
+            }
+            if (kind != K_LEN) {
+                ec = ST_INVALID_LITERAL_LENGTH;
+                h.mode = BAD;
+                goto quiet;
+            }
+            h.length = kLenBase[val];
+            h.extra = kLenExtra[val];
+            h.mode = LENEXT;
+        }
+            [[fallthrough]];
+        case LENEXT:
+            if (h.extra) {
+                if (!fill(h.extra)) goto done;
+                h.length += take(h.extra);
+            }
+            h.was = h.length;
+            h.mode = DIST;
+            [[fallthrough]];
+        case DIST: {
+            if (!fill(h.droot)) goto done;
+            uint32_t d = uni(L.tab[h.dtab + peek(h.droot)]);
+            if (is_link(d)) {
+                const uint32_t w = h.droot + slot_bits(d);
+                if (!fill(w)) goto done;
+                d = uni(L.tab[h.dtab + slot_val(d) + (peek(w) >> h.droot)]);
+                drop(h.droot + slot_bits(d));
+            } else {
+                drop(slot_bits(d));
+            }
+            if (slot_kind(d) != K_VAL) {
+                ec = ST_INVALID_DISTANCE_CODE;
+                h.mode = BAD;
+                goto quiet;
+            }
+            h.offset = kDistBase[slot_val(d)];
+            h.extra = kDistExtra[slot_val(d)];
+            h.mode = DISTEXT;
+        }
+            [[fallthrough]];
+        case DISTEXT:
+            if (h.extra) {
+                if (!fill(h.extra)) goto done;
+                h.offset += take(h.extra);
+            }
+            h.mode = MATCH;
+            [[fallthrough]];
+        case MATCH: {
+            if (op == cap) goto done;
+            uint64_t n = h.length;
+            if (h.offset > op) {   // from the window as it was when the call began
+                const uint32_t back = (uint32_t)(uint16_t)(h.offset - op);
+                if (back > h.wsize) {
+                    ec = ST_INVALID_DISTANCE;
+                    h.mode = BAD;
+                    goto quiet;
+                }
+                if (n > back) n = back;
+            }
+            if (n > cap - op) n = cap - op;
+            copy_back(h.offset, (uint32_t)n);
+            h.length -= (uint32_t)n;
+            if (h.length == 0) h.mode = LEN;
+            if (op - flushed >= FLUSH_AT) flush_out();
+            continue;
+        }
+        case LIT:
+            if (op == cap) goto done;
+            put(h.length);
+            h.mode = LEN;
+            continue;
+        case CHECK:
+            h.mode = DONE;
+            [[fallthrough]];
+        case DONE:
+            ec = ST_END_OF_STREAM;
+            goto done;
+        case BAD:
+            goto done;
+        default:   // SYNC: unreachable (the reference throws logic_error)
+            ec = ST_STREAM_ERROR;
+            goto quiet;
+        }
+    }
+
+done:   // the done() lambda, inflate_stream.ipp:88-119
+    flush_out();
+    if (op && h.mode < BAD && (h.mode < CHECK || flush != F_FINISH)) {
+        // window::write (window.hpp:109-141): the last min(n, capacity) bytes
+        const uint64_t k = op < wcap ? op : wcap;
+        for (uint64_t j = op - k + lane; j < op; j += WAVE)
+            st->win[(uint32_t)(h.wpos + j) & (wcap - 1)] = L.hist[(uint32_t)j & HM];
+        h.wpos = (uint32_t)((h.wpos + op) & (wcap - 1));
+        h.wsize = (uint32_t)((uint64_t)h.wsize + op < wcap ? h.wsize + op : wcap);
+    }
+    data_type = (int32_t)(bn + (h.last ? 64u : 0u) + (h.mode == TYPE ? 128u : 0u) +
+                          (h.mode == LEN_ || h.mode == COPY_ ? 256u : 0u));
+    if (((ip == 0 && op == 0) || flush == F_FINISH) && ec == 0) ec = ST_NEED_BUFFERS;
+    published = 1;
+quiet:
+    flush_out();
+    h.bv = bv;
+    h.bn = bn;
+    if (tab_dirty)
+        for (unsigned i = lane; i < kCodes; i += WAVE) st->codes[i] = L.tab[i];
+    if (lens_dirty)
+        for (unsigned i = lane; i < kLens; i += WAVE) st->lens[i] = L.lens[i];
+    if (lane == 0) {
+        st->h = h;
+        res->in_used = ip;
+        res->out_used = op;
+        res->ec = ec;
+        res->data_type = data_type;
+        res->published = published;
+    }
+}
+
+#ifndef BPMD_ZSTREAM_HOST
+__global__ void __launch_bounds__(WAVE)
+zstream_write_kernel(State* __restrict__ st, const uint8_t* __restrict__ in, uint64_t n_in, uint8_t* __restrict__ out,
+                     uint64_t cap, int flush, Result* __restrict__ res)
+{
+    __shared__ Lds L;
+    zstream_run(L, st, in, n_in, out, cap, flush, res);
+}
+#endif
+
+}  // namespace zst
+}  // namespace bpmd
+
+#ifndef BPMD_ZSTREAM_HOST
+// One inflate_stream::write() on `stream`: st is the stream's device state,
+// in/out device buffers of n_in bytes and `cap` bytes of room.
+extern "C" int bpmd_internal_zstream_write(void* st, const uint8_t* in, uint64_t n_in, uint8_t* out, uint64_t cap,
+                                           int flush, void* res, hipStream_t stream)
+{
+    using namespace bpmd::zst;
+    hipLaunchKernelGGL(zstream_write_kernel, dim3(1), dim3(bpmd::WAVE), 0, stream, (State*)st, in, n_in, out, cap,
+                       flush, (Result*)res);
+    return (int)hipGetLastError();
+}
+#endif

@@ -16,7 +16,10 @@
  * Beast's zlib::error values (include/boost/beast/zlib/error.hpp:48-138) in
  * the status array.  Device pointers refer to memory of the current HIP
  * device; `stream` is a hipStream_t (0 = default stream).  Batch calls are
- * asynchronous on `stream` and never allocate.
+ * asynchronous on `stream`; a call that needs device workspace (work queues,
+ * chunk scratch) takes it from a per-stream pool that the first such call on
+ * the stream allocates and a larger batch grows.  Concurrent calls from
+ * several host threads on one stream are serialised per stream.
  */
 #ifndef BEAST_PMD_H
 #define BEAST_PMD_H
@@ -222,9 +225,11 @@ int bpmd_inflate_takeover_batch(const bpmd_cfg* cfg, const uint8_t* d_in, const 
  * messages (do_context_takeover_write resets only under no_context_takeover,
  * impl_base.hpp:156-166), so its payloads may copy from earlier messages.
  * Message i's bytes at d_in + d_in_off[i] are preceded in d_in by
- * d_hist_len[i] bytes of that connection's earlier plaintext; matches reach
- * up to 4 KiB back into them (this engine's history window; the stream stays
- * valid for any windowBits >= 12 inflater).  Otherwise as bpmd_deflate_batch. */
+ * d_hist_len[i] bytes of that connection's earlier plaintext; a match reaches
+ * at most BPMD_CHUNK_HIST bytes (beast_amd/csrc/lz_core.h) before the 4 KiB
+ * chunk it is in and never more than 2^window_bits back, so the stream is
+ * valid for any inflater whose windowBits >= cfg->window_bits.  Otherwise as
+ * bpmd_deflate_batch. */
 int bpmd_deflate_takeover_batch(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_off,
                                 const uint32_t* d_in_len, const uint32_t* d_hist_len, uint32_t n_msgs,
                                 uint8_t* d_out, const uint64_t* d_out_off, const uint32_t* d_out_cap,
@@ -303,8 +308,9 @@ int bpmd_slide_batch(uint8_t* d_buf, const uint64_t* d_base, const uint32_t* d_p
 
 /* ---------------------------------------------------------------------
  * Per-stream API behind the C++ compatibility facade
- * (include/beast_amd/zlib.hpp).  Host buffers; each call runs the batch
- * kernels on the current device for one message and synchronises.
+ * (include/boost/beast/zlib/ headers).  Host buffers; each call runs on the
+ * current device (deflate: the batch kernels on one message; inflate: the
+ * per-stream kernel) and synchronises.
  * Throughput comes from the batch API above; these calls exist so code
  * written against zlib::deflate_stream / zlib::inflate_stream (the calls
  * impl_base<true> makes, impl_base.hpp:85-190) runs unchanged.
@@ -355,14 +361,17 @@ int bpmd_inflate_stream_create(int window_bits, bpmd_stream** out);
 int bpmd_inflate_stream_reset(bpmd_stream* s, int window_bits);
 /* inflate_stream::clear() -- a no-op in the reference (inflate_stream.ipp:49-53) */
 int bpmd_inflate_stream_clear(bpmd_stream* s);
-/* inflate_stream::write(zs, flush, ec) (inflate_stream.ipp:74-535).  A
- * resumable decoder: each call decodes its own input (plus at most one
- * decode round again) from the checkpoint the previous call left, with the
- * window of the last 2^windowBits output bytes kept on the device; input is
- * reported consumed whole (kept until decoded when avail_out runs out). */
+/* inflate_stream::write(zs, flush, ec) (inflate_stream.ipp:74-535).  The
+ * reference's decoder state (mode, bit reservoir, tables, 2^windowBits
+ * window) lives on the device and each call runs its state machine there
+ * (beast_amd/csrc/pmd_zstream.hip), so the status, the output bytes and
+ * every z_params field -- next_in/avail_in/total_in included: input the
+ * reference leaves unconsumed stays with the caller -- equal Beast's after
+ * every call.  A data error returns without advancing z_params, as the
+ * reference's err() does (inflate_stream.ipp:120-125). */
 int bpmd_inflate_stream_write(bpmd_stream* s, bpmd_zparams* zs, int flush);
-/* Memory an inflate stream holds (host: kept input; device: window, output
- * slot and input buffers); no reference counterpart, for bounded-memory tests. */
+/* Memory an inflate stream holds (host: none; device: state + window and the
+ * call's input/output buffers); no reference counterpart, for bounded-memory tests. */
 int bpmd_inflate_stream_footprint(const bpmd_stream* s, size_t* host_bytes, size_t* device_bytes);
 void bpmd_stream_destroy(bpmd_stream* s);
 

@@ -1,8 +1,9 @@
 // boost/beast/zlib/inflate_stream.hpp -- drop-in zlib::inflate_stream
 // (reference: include/boost/beast/zlib/inflate_stream.hpp:63-213) backed by
-// the MI355X engine's resumable per-stream decoder (bpmd_inflate_stream_*,
-// include/beast_pmd.h; beast_amd/csrc/inflate_resume.h).  Output bytes and
-// zlib::error values are the reference's; reset() throws std::domain_error
+// the MI355X engine's per-stream decoder (bpmd_inflate_stream_*,
+// include/beast_pmd.h; the state machine runs on the device,
+// beast_amd/csrc/pmd_zstream.hip).  Output bytes, zlib::error values and
+// every z_params field after each write() are the reference's; reset() throws std::domain_error
 // for windowBits outside 8..15 (inflate_stream.ipp:57-61); clear() keeps
 // the window and state as the reference's (empty) doClear does.
 #ifndef BOOST_BEAST_ZLIB_INFLATE_STREAM_HPP

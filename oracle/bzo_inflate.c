@@ -431,8 +431,9 @@ bad:
 static const uint8_t clen_order[19] = {
     16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
-/* Error exits at inflate_stream.ipp:338-350 and :362-366 return without the
- * done() bookkeeping: zs and the window are left untouched. */
+/* Error exits -- err() (inflate_stream.ipp:120-125), the table errors at
+ * :336-349 and inflate_fast's at :362-369 -- return without the done()
+ * bookkeeping: zs and the window are left untouched. */
 static int quiet_fail(bzo_inflater* s, cursor_t* c, int err)
 {
     s->mode = M_BAD;
@@ -474,7 +475,9 @@ int bzo_inflate_write(bzo_inflater* s, bzo_zparams* zs, int flush)
     int ec = 0;
 
 #define NEED(n) do { if (!bits_need(b, (n), &c.in, c.in_end)) return finish_call(s, zs, &c, flush, ec); } while (0)
-#define FAIL(e) do { ec = (e); s->mode = M_BAD; return finish_call(s, zs, &c, flush, ec); } while (0)
+/* err() (inflate_stream.ipp:120-125) sets BAD and returns without done():
+ * z_params are not advanced, though the bytes are in the caller's buffer */
+#define FAIL(e) return quiet_fail(s, &c, (e))
 
     if (s->mode == M_TYPE) s->mode = M_TYPEDO;
     for (;;) {
