@@ -9,6 +9,7 @@
 #ifndef BOOST_BEAST_ZLIB_ERROR_HPP
 #define BOOST_BEAST_ZLIB_ERROR_HPP
 
+#include <cstddef>
 #include <string>
 #include <system_error>
 #include <type_traits>
@@ -58,14 +59,23 @@ enum class error
 
 namespace detail {
 
+// impl/error.ipp:47-115.  boost::system::error_category has the buffer form
+// of message() as a virtual; std::error_category does not, so there it is a
+// plain member with the same meaning.
+#ifdef BPMD_ZLIB_BOOST_SYSTEM
+#define BPMD_ZLIB_MESSAGE_BUF_OVERRIDE override
+#else
+#define BPMD_ZLIB_MESSAGE_BUF_OVERRIDE
+#endif
+
 class error_codes : public boost::beast::error_category
 {
 public:
     const char* name() const noexcept override { return "boost.beast.zlib"; }
 
-    std::string message(int ev) const override
+    // impl/error.ipp:57-86
+    char const* message(int ev, char*, std::size_t) const noexcept BPMD_ZLIB_MESSAGE_BUF_OVERRIDE
     {
-        // impl/error.ipp:31-58
         switch (static_cast<error>(ev)) {
         case error::need_buffers: return "need buffers";
         case error::end_of_stream: return "unexpected end of deflate stream";
@@ -85,6 +95,27 @@ public:
         case error::general:
         default: return "beast.zlib error";
         }
+    }
+
+    // impl/error.ipp:88-92
+    std::string message(int ev) const override { return message(ev, nullptr, 0); }
+
+    // impl/error.ipp:94-98
+    boost::beast::error_condition default_error_condition(int ev) const noexcept override
+    {
+        return boost::beast::error_condition{ev, *this};
+    }
+
+    // impl/error.ipp:100-106
+    bool equivalent(int ev, boost::beast::error_condition const& condition) const noexcept override
+    {
+        return condition.value() == ev && &condition.category() == this;
+    }
+
+    // impl/error.ipp:108-113
+    bool equivalent(boost::beast::error_code const& error, int ev) const noexcept override
+    {
+        return error.value() == ev && &error.category() == this;
     }
 };
 

@@ -36,9 +36,20 @@ def _build(name):
     return out
 
 
-@pytest.mark.parametrize("name", ["facade_roundtrip", "ws_echo"])
+@pytest.mark.parametrize("name", ["facade_roundtrip", "ws_echo", "write_threshold"])
 def test_facade_compiles_and_links(name):
     assert os.path.exists(_build(name))
+
+
+def test_impl_base_codec_uses_compile():
+    """Every codec use of websocket/detail/impl_base.hpp (restated in
+    tests/cpp/impl_base_codec.cpp with the reference's types, members,
+    enumerators and error comparisons) compiles against the drop-in headers,
+    including the error category's impl/error.ipp:47-115 overrides."""
+    src = os.path.join(CPP, "impl_base_codec.cpp")
+    r = subprocess.run(["g++", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-fsyntax-only", "-I",
+                        os.path.join(ROOT, "include"), src], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
 
 
 def test_without_gpu_engine_reports_instead_of_falling_back():
@@ -63,3 +74,19 @@ def test_c1_loopback_echo_on_gpu():
     assert r.returncode == 0, r.stdout + r.stderr
     assert "echo ok: 1024 messages x 1024 B" in r.stdout, r.stdout
     print(r.stdout)
+
+
+def test_msg_size_threshold_decisions():
+    """write.cpp:659-739 (issues 226, 227): begin_msg's compress decision
+    through compress_message; a message sent raw costs more than its size."""
+    r = subprocess.run([_build("write_threshold"), "cpu"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_msg_size_threshold_on_gpu():
+    """write.cpp:659-807 incl. issue 1666: with the default threshold the
+    256-byte message goes through zlib::deflate_stream on the GPU and costs
+    fewer bytes than its size."""
+    r = subprocess.run([_build("write_threshold"), "gpu"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "issue1666" in r.stdout, r.stdout + r.stderr
