@@ -110,14 +110,17 @@ def cpu_baselines(comp_buf, comp_off, comp_len, raw_lens, raw3, off3, len3, targ
     of Beast's zlib ("port", byte-identical to Beast at L1-9) and the
     reference's own zlib 1.3.1 ("reference", compiled from
     test/extern/zlib-1.3.1 by oracle/Makefile) and, as an extra column, the
-    image's system zlib behind the same shim ("system"), each at 1 thread and at T
-    threads = the cores this process may use (capped at 16, the box's share
-    for one GPU).  Per measurement the sample is sized for ~target_s of CPU
-    work; median of 3, outputs preallocated (oracle.time_batch)."""
+    image's system zlib behind the same shim ("system"), each at 1 thread, 16
+    threads and T = 32 threads (the per-GPU share of an 8-GPU node's 256
+    hardware threads), capped at the cores this process may use.  Per
+    measurement the sample is sized for ~target_s of CPU work; median of 3,
+    outputs preallocated (oracle.time_batch)."""
     from oracle import oracle as O
     cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    T = max(1, min(cores, 16))
-    out = {"cpu_model": _cpu_model(), "nproc": os.cpu_count(), "cores_available": cores, "threads": T}
+    T = max(1, min(cores, 32))
+    T16 = max(1, min(cores, 16))
+    out = {"cpu_model": _cpu_model(), "nproc": os.cpu_count(), "cores_available": cores, "threads": T,
+           "threads_16": T16}
     n = len(comp_len)
     ub = np.full(n, pmd.upper_bound(MSG_BYTES) + 16, dtype=np.uint32)
 
@@ -139,8 +142,9 @@ def cpu_baselines(comp_buf, comp_off, comp_len, raw_lens, raw3, off3, len3, targ
         for impl in ("port", "reference", "system"):
             one = leg(impl, inflate, 1)
             many = leg(impl, inflate, T) if one else None
+            mid = leg(impl, inflate, T16) if one and T16 != T else many
             if one:
-                r[impl] = {"1_thread": one["value"], f"{T}_threads": many["value"],
+                r[impl] = {"1_thread": one["value"], f"{T16}_threads": mid["value"], f"{T}_threads": many["value"],
                            "sample_1": f"{one['msgs']} msgs", f"sample_{T}": f"{many['msgs']} msgs"}
                 if not inflate and impl == "port":
                     r["_beast_len"] = many["out_len"]
@@ -198,6 +202,49 @@ def pmc_traffic(kernel):
                                    "write_bytes": int(wb), "fetch_factor": factor, "fetch_calibration": calib}
 
 
+# the kernel one step of each profiled op launches once (its launch count is
+# the number of steps in the PMC pass)
+LEG_ANCHOR = {("c3", "deflate"): "deflate_kernel", ("c4_l6", "deflate"): "stitch_kernel",
+              ("c4_l6", "inflate"): "inflate_lane3_kernel", ("c5_l1", "deflate"): "stitch_kernel",
+              ("c5_l1", "inflate"): "inflate_kernel", ("c5_l6", "deflate"): "stitch_kernel",
+              ("c5_l6", "inflate"): "inflate_kernel"}
+
+
+def pmc_traffic_leg(leg, op):
+    """HBM bytes per step of one op of a bench leg, from the newest PMC
+    summary of scripts/leg_profile.py (profiles/rNN_<leg>_<op>_pmc.csv: every
+    non-torch kernel of that op, FETCH_SIZE and WRITE_SIZE in separate passes)
+    with the FETCH_SIZE calibration factor.  Returns (bytes, details) or None."""
+    import csv
+    f = _newest(f"r*_{leg}_{op}_pmc.csv")
+    if not f:
+        return None
+    fetch = write = 0.0
+    anchors = 0
+    with open(f) as fh:
+        for r in csv.DictReader(fh):
+            k = r["kernel"].split("::")[-1].split("<")[0]
+            v = float(r["value_kB"]) * 1024
+            if r["counter"] == "FETCH_SIZE":
+                fetch += v
+                anchors += k == LEG_ANCHOR[(leg, op)]
+            else:
+                write += v
+    if not anchors:
+        return None
+    factor = 1.0
+    c = _newest("r*_fetch_calib.csv")
+    if c:
+        with open(c) as fh:
+            for r in csv.DictReader(fh):
+                if r["pattern"] == "coalesced_16B":
+                    factor = float(r["bytes_per_counted_byte"])
+    per = (fetch * factor + write) / anchors
+    return int(per), {"source": os.path.relpath(f, ROOT), "steps": anchors,
+                      "fetch_bytes_raw_per_step": int(fetch / anchors), "write_bytes_per_step": int(write / anchors),
+                      "fetch_factor": factor}
+
+
 class Timer:
     """K timed steps bracketed by barrier + synchronize; per-step HIP events
     on the launch stream for the kernel-side average."""
@@ -223,7 +270,9 @@ class Timer:
             self.dist.barrier()
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
-        kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+        # per-step HIP event times on the launch stream, median over the
+        # timed steps (the warmup's cold launch is not among them)
+        kern_ms = float(np.median([a.elapsed_time(b) for a, b in ev]))
         if self.dist:
             t = torch.tensor([wall, kern_ms], dtype=torch.float64, device="cuda")
             self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
@@ -244,6 +293,21 @@ def shard_config(lens_all, rank, world):
     return s0, e0, [int(np.asarray(lens_all[a:b], dtype=np.int64).sum()) for a, b in ranges]
 
 
+def roofline(alg_bytes, kern_ms, kernels, traffic=None):
+    """`roofline` object: algorithmic bytes of one launch (or one step of
+    several launches) over its HIP-event time on the launch stream."""
+    a = alg_bytes / (kern_ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(a, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(a / HBM_PEAK_GBS, 5), "traffic": traffic[0] if traffic else None,
+            "traffic_source": traffic[1] if traffic else None, "kernel": kernels,
+            "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": int(alg_bytes)}
+
+
+DEFLATE_STEP_KERNELS = "deflate_kernel + count_chunks + scan + fill_items + deflate_chunks + stitch"
+INFLATE_STEP_KERNELS = {"c4_l6": "order_keys + radix sort + inflate_lane3_kernel (work queue)",
+                        "c5_l1": "inflate_kernel (wave per message)", "c5_l6": "inflate_kernel (wave per message)"}
+
+
 def mixed_legs(args, rank, world, timer, dev):
     """configs[3] (C4: Zipf 256 B-64 KiB JSON, L6/mem4) and configs[4] (C5: 64 KiB
     low-compressibility binary, L1 and L6).  Each config is ONE global batch,
@@ -252,13 +316,19 @@ def mixed_legs(args, rank, world, timer, dev):
     its own range (seeded by global message index), deflates it on its GPU,
     inflates the payloads back and checks them byte for byte on the device.
     No payload crosses ranks.  Values are GiB/s of uncompressed bytes of the
-    whole batch over the max-over-ranks time (strong scaling)."""
+    whole batch over the max-over-ranks time (strong scaling); each step's
+    roofline is its algorithmic bytes over the step's HIP-event time (all of
+    its kernels).  At N=1, "virtual_shards" runs every rank's share of an
+    N = 2, 4, 8 split alone on this GPU and projects the N-GPU aggregate from
+    the slowest share (each rank of a real node has a whole GPU too)."""
     steps = max(1, min(args.steps, 3))
     out = {"steps": steps, "unit": "GiB/s", "scaling": "strong"}
     c4_all = synth.zipf_sizes(args.c4_msgs, SEED_C4)
     c5_all = np.full(args.c5_msgs, 65536, dtype=np.uint32)
     legs = [("c4_l6", "json", c4_all, SEED_C4, 6), ("c5_l1", "binary", c5_all, SEED_C5, 1),
             ("c5_l6", "binary", c5_all, SEED_C5, 6)]
+    if args.legs:
+        legs = [l for l in legs if l[0] in args.legs.split(",")]
     batches = {}
     for name, kind, lens_all, seed, level in legs:
         s0, e0, per_rank = shard_config(lens_all, rank, world)
@@ -277,16 +347,18 @@ def mixed_legs(args, rank, world, timer, dev):
         coff = pmd.slot_offsets(cap)
         cbuf = torch.empty(int(coff[-1].item()) + int(cap[-1].item()) + 64, dtype=torch.uint8, device=dev)
 
-        def deflate_step():
-            return pmd.deflate_batch(src, level=level, mem_level=4, out_cap=cap, out=cbuf, out_off=coff)
+        def deflate_step(a=0, b=len(lens)):
+            sub = src if (a, b) == (0, len(lens)) else pmd.Batch(src.data, src.off[a:b], src.len[a:b])
+            return pmd.deflate_batch(sub, level=level, mem_level=4, out_cap=cap[a:b], out=cbuf, out_off=coff[a:b])
 
         d = deflate_step()
         torch.cuda.synchronize()
         comp = pmd.Batch(cbuf, coff, d.out.len.clone())
         rbuf = torch.empty_like(src.data)
 
-        def inflate_step():
-            return pmd.inflate_batch(comp, src.len, out=rbuf, out_off=src.off)
+        def inflate_step(a=0, b=len(lens)):
+            sub = comp if (a, b) == (0, len(lens)) else pmd.Batch(cbuf, coff[a:b], comp.len[a:b])
+            return pmd.inflate_batch(sub, src.len[a:b], out=rbuf, out_off=src.off[a:b])
 
         r = inflate_step()
         torch.cuda.synchronize()
@@ -294,15 +366,35 @@ def mixed_legs(args, rank, world, timer, dev):
               and torch.equal(r.out.len, src.len) and torch.equal(rbuf[:total], src.data[:total]))
         if not ok:
             log(f"[rank {rank}] {name} ROUND-TRIP FAILURE")
-        d_step, _ = timer.run(deflate_step, steps, 1)
-        i_step, _ = timer.run(inflate_step, steps, 1)
+        d_step, d_kern = timer.run(deflate_step, steps, 1)
+        i_step, i_kern = timer.run(inflate_step, steps, 1)
         comp_bytes = int(d.out.len.to(torch.int64).sum())
+        alg = total + comp_bytes + 16 * len(lens)
         out[name] = {"msgs": len(lens_all), "bytes": total_all, "msgs_rank0": int(e0 - s0) if rank == 0 else None,
                      "bytes_per_rank": per_rank,
                      "imbalance_max_over_min": round(max(per_rank) / max(1, min(per_rank)), 4),
                      "deflate_value": round(total_all / (1 << 30) / d_step, 3),
                      "inflate_value": round(total_all / (1 << 30) / i_step, 3),
+                     "deflate_roofline": roofline(alg, d_kern, DEFLATE_STEP_KERNELS, pmc_traffic_leg(name, "deflate")),
+                     "inflate_roofline": roofline(alg, i_kern, INFLATE_STEP_KERNELS[name],
+                                                  pmc_traffic_leg(name, "inflate")),
                      "ratio_rank_local": round(comp_bytes / max(1, total), 4), "roundtrip_ok": bool(ok)}
+        if world == 1 and not args.no_virtual_shards:
+            from beast_amd import shard
+            vs = {}
+            for parts in (2, 4, 8):
+                dt, it = [], []
+                for a, b in shard.byte_balanced_ranges(lens, parts):
+                    dt.append(timer.run(lambda: deflate_step(a, b), steps, 1)[0])
+                    it.append(timer.run(lambda: inflate_step(a, b), steps, 1)[0])
+                vs[str(parts)] = {
+                    "deflate_shard_ms": [round(t * 1e3, 3) for t in dt],
+                    "inflate_shard_ms": [round(t * 1e3, 3) for t in it],
+                    "deflate_projected_value": round(total / (1 << 30) / max(dt), 3),
+                    "inflate_projected_value": round(total / (1 << 30) / max(it), 3),
+                    "deflate_projected_speedup": round(d_step / max(dt), 3),
+                    "inflate_projected_speedup": round(i_step / max(it), 3)}
+            out[name]["virtual_shards"] = vs
         del cbuf, rbuf, comp, d, r
     return out
 
@@ -318,6 +410,9 @@ def main():
     ap.add_argument("--no-deflate", action="store_true")
     ap.add_argument("--no-frame", action="store_true")
     ap.add_argument("--no-mixed", action="store_true")
+    ap.add_argument("--legs", default="", help="comma list of mixed legs to run (c4_l6,c5_l1,c5_l6); default all")
+    ap.add_argument("--no-virtual-shards", action="store_true",
+                    help="skip the N=1 per-shard timing that projects the 2/4/8-GPU aggregate")
     ap.add_argument("--c4-msgs", type=int, default=C4_MSGS, help="configs[3] batch (all ranks together)")
     ap.add_argument("--c5-msgs", type=int, default=C5_MSGS, help="configs[4] batch (all ranks together)")
     args = ap.parse_args()
@@ -516,9 +611,7 @@ def main():
             "inflate_of_gpu_payloads_value": round(uncomp * world / (1 << 30) / i_step, 3),
             "unit": "GiB/s", "roundtrip_ok": bool(ok3),
             "ratio": round(comp3 / uncomp, 4),
-            "roofline": {"bound": "hbm", "achieved": round(dalg / (d_kern * 1e-3) / 1e9, 2), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(dalg / (d_kern * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
-                         "kernel": "deflate_kernel", "kernel_ms": round(d_kern, 4), "alg_bytes_per_launch": dalg},
+            "roofline": roofline(dalg, d_kern, "deflate_kernel", pmc_traffic_leg("c3", "deflate")),
         }
         exact_len = None
         if not args.no_exact:
@@ -550,6 +643,7 @@ def main():
                 T = cpu["threads"]
                 result["deflate"]["cpu_baseline"] = {
                     "value": dcpu["port"][f"{T}_threads"], "unit": "GiB/s", "cores": T, "kind": "port",
+                    "value_16_threads": dcpu["port"][f"{cpu['threads_16']}_threads"],
                     "sample": f"C3 messages, {dcpu['port'][f'sample_{T}']}, L6/mem4/w15 + pmd framing",
                     "one_thread": dcpu["port"]["1_thread"], "reference_zlib_1.3.1": dcpu.get("reference"),
                     "system_zlib": dcpu.get("system")}
@@ -567,6 +661,7 @@ def main():
         if "port" in icpu:
             result["cpu_baseline"] = {
                 "value": icpu["port"][f"{T}_threads"], "unit": "GiB/s", "cores": T, "kind": "port",
+                "value_16_threads": icpu["port"][f"{cpu['threads_16']}_threads"],
                 "sample": f"C2 payloads, {icpu['port'][f'sample_{T}']} x {MSG_BYTES} B, oracle inflate "
                           f"(C restatement of Beast's zlib), {T} threads, median of 3",
                 "one_thread": icpu["port"]["1_thread"], "reference_zlib_1.3.1": icpu.get("reference"),

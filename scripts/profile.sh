@@ -25,5 +25,6 @@ python3 $ROOT/scripts/pmc_summary.py $(find $OUT -name 'fetch_counter_collection
   $(find $OUT -name 'write_counter_collection.csv') > $OUT/c2_pmc.csv || exit 6
 python3 $ROOT/scripts/fetch_calib_summary.py $(find $OUT -name 'calib_counter_collection.csv') \
   > $OUT/fetch_calib.csv || exit 7
-cp $(find $OUT -name 'trace_kernel_stats.csv' | head -1) $OUT/c2_kernel_stats.csv
+cp $(find $OUT -name "trace_kernel_stats.csv" | head -1) $OUT/c2_kernel_stats.csv
+python3 $ROOT/scripts/kernel_summary.py $(find $OUT -name "trace_kernel_trace.csv" | head -1) > $OUT/c2_kernels.csv || exit 8
 echo done
