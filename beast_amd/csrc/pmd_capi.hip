@@ -131,7 +131,7 @@ uint8_t* scratch_for(hipStream_t s, size_t bytes, int which = 0)
 
 // scratch block `which` (0 inflate queue, 1-2 deflate workspace, 3-4 exact
 // deflate queue and workspace, 5 inflate message order, 6 wave inflate queue,
-// 7 deflate chunk queue) for other translation units
+// 7 deflate chunk queue, 8 multi-device output totals) for other translation units
 extern "C" void* bpmd_internal_scratch(hipStream_t s, size_t bytes, int which)
 {
     return scratch_for(s, bytes, which);

@@ -61,6 +61,9 @@ def lib():
         L.bpmd_inflate_batch.argtypes = [ctypes.POINTER(_Cfg), vp, vp, vp, ctypes.c_uint32, vp, vp, vp, vp, vp, vp]
         L.bpmd_inflate_batch.restype = ctypes.c_int
         L.bpmd_deflate_batch.argtypes = [ctypes.POINTER(_Cfg), vp, vp, vp, ctypes.c_uint32, vp, vp, vp, vp, vp, vp]
+        L.bpmd_shard_ranges.argtypes = [vp, ctypes.c_uint32, ctypes.c_int, vp]
+        L.bpmd_inflate_batch_multi.argtypes = [ctypes.POINTER(_Cfg), vp, ctypes.c_int, vp]
+        L.bpmd_deflate_batch_multi.argtypes = [ctypes.POINTER(_Cfg), vp, ctypes.c_int, vp]
         L.bpmd_deflate_batch.restype = ctypes.c_int
         u32 = ctypes.c_uint32
         L.bpmd_mask_batch.argtypes = [vp, vp, vp, u32, vp, vp, vp]
@@ -601,3 +604,69 @@ class TakeoverDeflater:
                                              _ptr(status), _stream_handle(stream)), "bpmd_deflate_takeover_batch")
         self.pos[conn] = pos + lens
         return Result(Batch(out, out_off, out_len), cap, status)
+
+
+# ------------------------------------------------- one process, several GPUs
+
+class _Shard(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int), ("stream", ctypes.c_void_p), ("d_in", ctypes.c_void_p),
+                ("d_in_off", ctypes.c_void_p), ("d_in_len", ctypes.c_void_p), ("n_msgs", ctypes.c_uint32),
+                ("d_out", ctypes.c_void_p), ("d_out_off", ctypes.c_void_p), ("d_out_cap", ctypes.c_void_p),
+                ("d_out_len", ctypes.c_void_p), ("d_status", ctypes.c_void_p)]
+
+
+def shard_ranges(lens, n_parts: int):
+    """bpmd_shard_ranges: [(start, end)] byte-balanced contiguous ranges."""
+    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    starts = np.zeros(n_parts + 1, dtype=np.uint32)
+    _check(lib().bpmd_shard_ranges(lens.ctypes.data_as(ctypes.c_void_p), len(lens), n_parts,
+                                   starts.ctypes.data_as(ctypes.c_void_p)), "bpmd_shard_ranges")
+    return [(int(starts[i]), int(starts[i + 1])) for i in range(n_parts)]
+
+
+def _multi(fn, cfg, parts):
+    """parts: [(src Batch, out buffer, out_off, cap, out_len, status, stream)]."""
+    arr = (_Shard * len(parts))()
+    for i, (src, out, out_off, cap, out_len, status, stream) in enumerate(parts):
+        arr[i] = _Shard(src.data.device.index or 0, _stream_handle(stream), _ptr(src.data), _ptr(src.off),
+                        _ptr(src.len), src.n, _ptr(out), _ptr(out_off), _ptr(cap), _ptr(out_len), _ptr(status))
+    totals = np.zeros(len(parts), dtype=np.uint64)
+    _check(fn(ctypes.byref(cfg), arr, len(parts), totals.ctypes.data_as(ctypes.c_void_p)), fn.__name__)
+    return totals
+
+
+def inflate_batch_multi(srcs, out_caps, window_bits: int = 15, streams=None):
+    """bpmd_inflate_batch_multi over shards (each a Batch on its own device):
+    returns ([Result], per-shard output byte totals)."""
+    streams = streams or [None] * len(srcs)
+    parts, res = [], []
+    for src, c, st in zip(srcs, out_caps, streams):
+        dev = src.data.device
+        cap = torch.full((src.n,), c, dtype=torch.int32, device=dev) if isinstance(c, int) else c.to(dev)
+        off = slot_offsets(cap)
+        out = torch.empty((int(off[-1].item() + cap[-1].item()) if src.n else 0) + 16, dtype=torch.uint8, device=dev)
+        out_len = torch.empty(src.n, dtype=torch.int32, device=dev)
+        status = torch.empty(src.n, dtype=torch.int32, device=dev)
+        parts.append((src, out, off, cap, out_len, status, st))
+        res.append(Result(Batch(out, off, out_len), cap, status))
+    totals = _multi(lib().bpmd_inflate_batch_multi, _Cfg(0, window_bits, 8, 0, 0), parts)
+    return res, totals
+
+
+def deflate_batch_multi(srcs, level: int = 6, window_bits: int = 15, mem_level: int = 4, strategy: int = 0,
+                        streams=None):
+    """bpmd_deflate_batch_multi over shards; slots of deflate_upper_bound."""
+    streams = streams or [None] * len(srcs)
+    parts, res = [], []
+    for src, st in zip(srcs, streams):
+        dev = src.data.device
+        l64 = src.len.to(torch.int64)
+        cap = (l64 + (l64 + 7) // 8 + (l64 + 63) // 64 + 11).to(torch.int32)
+        off = slot_offsets(cap)
+        out = torch.empty((int(off[-1].item() + cap[-1].item()) if src.n else 0) + 16, dtype=torch.uint8, device=dev)
+        out_len = torch.empty(src.n, dtype=torch.int32, device=dev)
+        status = torch.empty(src.n, dtype=torch.int32, device=dev)
+        parts.append((src, out, off, cap, out_len, status, st))
+        res.append(Result(Batch(out, off, out_len), cap, status))
+    totals = _multi(lib().bpmd_deflate_batch_multi, _Cfg(level, window_bits, mem_level, strategy, 0), parts)
+    return res, totals

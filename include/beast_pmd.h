@@ -134,6 +134,44 @@ int bpmd_set_inflate_kernel(int mode);
 size_t bpmd_deflate_upper_bound(size_t n);
 
 /* ---------------------------------------------------------------------
+ * One process, several GPUs.  Messages are
+ * independent streams, so a batch splits into contiguous, byte-balanced
+ * message ranges, one per device; every shard's buffers live on its own
+ * device and no payload crosses GPUs.
+ * ------------------------------------------------------------------- */
+
+/* Byte-balanced contiguous ranges (beast_amd/shard.py): shard p is messages
+ * [starts[p], starts[p+1]), starts has n_parts + 1 entries; shard r ends at
+ * the first message whose byte prefix sum reaches (r + 1) / n_parts of the
+ * total.  Host only. */
+int bpmd_shard_ranges(const uint32_t* lens, uint32_t n, int n_parts, uint32_t* starts);
+
+/* One shard: device pointers of `device`, launched on `stream` (a
+ * hipStream_t of that device, 0 = its default stream). */
+typedef struct bpmd_shard {
+    int device;
+    void* stream;
+    const uint8_t* d_in;
+    const uint64_t* d_in_off;
+    const uint32_t* d_in_len;
+    uint32_t n_msgs;
+    uint8_t* d_out;
+    const uint64_t* d_out_off;
+    const uint32_t* d_out_cap;
+    uint32_t* d_out_len;
+    int32_t* d_status;
+} bpmd_shard;
+
+/* bpmd_inflate_batch / bpmd_deflate_batch on every shard, each on its own
+ * device and stream, asynchronously.  out_bytes (n_shards entries, or NULL):
+ * each shard's total output bytes (sum of its d_out_len), gathered to the
+ * host -- the call then waits for every shard -- so each shard's offset in
+ * one global output is the exclusive prefix sum.  The current device is
+ * restored. */
+int bpmd_inflate_batch_multi(const bpmd_cfg* cfg, const bpmd_shard* shards, int n_shards, uint64_t* out_bytes);
+int bpmd_deflate_batch_multi(const bpmd_cfg* cfg, const bpmd_shard* shards, int n_shards, uint64_t* out_bytes);
+
+/* ---------------------------------------------------------------------
  * Frame-adjacent byte passes.  Masking keys are the
  * frame header's 32-bit key as Beast reads it, little-endian from the wire
  * (stream_impl.hpp:866-870): payload byte j is XORed with byte (j + phase) % 4

@@ -127,3 +127,16 @@ def test_two_rank_gloo_runs_bench_partition():
     assert max(b0) - min(b0) <= 2 * int(lens_all.max())
     assert st0 == 0 and st1 == len(out0) and tot0 == tot1 == len(expect)
     assert out0 + out1 == expect   # per-rank synthesis by global index == the whole batch
+
+
+def test_c_abi_shard_ranges_match_python():
+    """bpmd_shard_ranges (the C++ server's split, pmd_multi.hip) cuts exactly
+    where beast_amd/shard.py does."""
+    from beast_amd import pmd, synth
+    rng = np.random.default_rng(5)
+    cases = [synth.zipf_sizes(20000, 0x5EED0004), np.full(1000, 65536, dtype=np.uint32),
+             np.zeros(17, dtype=np.uint32), np.array([], dtype=np.uint32), np.array([7], dtype=np.uint32),
+             rng.integers(0, 70000, 5000).astype(np.uint32)]
+    for lens in cases:
+        for world in (1, 2, 3, 4, 7, 8):
+            assert pmd.shard_ranges(lens, world) == shard.byte_balanced_ranges(lens, world), (len(lens), world)
