@@ -27,8 +27,16 @@ extern "C" int bpmd_internal_inflate_lane3(const uint8_t* in, const uint64_t* in
                                            uint32_t* out_len, int32_t* status, uint32_t raw, const uint32_t* mask_key,
                                            const uint32_t* hist_len, uint32_t hist_max, uint32_t max_in,
                                            const uint32_t* order, uint32_t* qctr, uint32_t grid_wgs,
-                                           hipStream_t stream);
-extern "C" const uint32_t* bpmd_internal_lane_order(const uint32_t* in_len, uint32_t n, hipStream_t stream);
+                                           const uint32_t* skip, hipStream_t stream);
+extern "C" const uint32_t* bpmd_internal_lane_order(const uint32_t* in_len, uint32_t n, hipStream_t stream,
+                                                    const uint32_t** keys_out);
+extern "C" const uint32_t* bpmd_internal_lane_long_split(const uint32_t* in_len, const uint32_t* keys, uint32_t n,
+                                                         uint32_t lanes, hipStream_t stream);
+extern "C" int bpmd_internal_inflate_wave_ordered(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                                  uint32_t n, uint8_t* out, const uint64_t* out_off,
+                                                  const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
+                                                  uint32_t raw, const uint32_t* mask_key, const uint32_t* order,
+                                                  const uint32_t* limit, hipStream_t stream);
 extern "C" int bpmd_internal_deflate_keyed(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                            uint32_t n, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                                            uint32_t* out_len, int32_t* status, int level, int window_bits,
@@ -131,7 +139,8 @@ uint8_t* scratch_for(hipStream_t s, size_t bytes, int which = 0)
 
 // scratch block `which` (0 inflate queue, 1-2 deflate workspace, 3-4 exact
 // deflate queue and workspace, 5 inflate message order, 6 wave inflate queue,
-// 7 deflate chunk queue, 8 multi-device output totals) for other translation units
+// 7 deflate chunk queue, 8 multi-device output totals, 9 long-payload split)
+// for other translation units
 extern "C" void* bpmd_internal_scratch(hipStream_t s, size_t bytes, int which)
 {
     return scratch_for(s, bytes, which);
@@ -276,6 +285,7 @@ int inflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
         if (q_override) wgs = q_override;
         uint32_t* qctr = nullptr;
         const uint32_t* order = nullptr;
+        const uint32_t* nlong = nullptr;
         if (n_msgs > wgs * 64u && !split) {
             qctr = (uint32_t*)scratch_for(s, 256);
             if (!qctr || hipMemsetAsync(qctr, 0, sizeof(uint32_t), s) != hipSuccess) return BPMD_R_HIP_ERROR;
@@ -285,11 +295,24 @@ int inflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
                 const char* e = getenv("BPMD_INFLATE_ORDER");
                 return !(e && e[0] == '0');
             }();
-            if (ordered && !(order = bpmd_internal_lane_order(d_in_len, n_msgs, s))) return BPMD_R_HIP_ERROR;
+            // payloads too long for one lane go to the wave kernel first
+            // (automatic mode, no takeover window; BPMD_INFLATE_LONG=0: off)
+            static const bool long_split = [] {
+                const char* e = getenv("BPMD_INFLATE_LONG");
+                return !(e && e[0] == '0');
+            }();
+            const uint32_t* keys = nullptr;
+            if (ordered && !(order = bpmd_internal_lane_order(d_in_len, n_msgs, s, &keys))) return BPMD_R_HIP_ERROR;
+            if (ordered && long_split && m == 0 && !hist) {
+                if (!(nlong = bpmd_internal_lane_long_split(d_in_len, keys, n_msgs, wgs * 64u, s)) ||
+                    bpmd_internal_inflate_wave_ordered(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap,
+                                                       d_out_len, d_status, raw, key, order, nlong, s))
+                    return BPMD_R_HIP_ERROR;
+            }
         }
         e = bpmd_internal_inflate_lane3(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
                                         d_status, raw, key, hist, 1u << cfg->window_bits, split, order, qctr, wgs,
-                                        s);
+                                        nlong, s);
     }
     if (!e && (!lane || split))
         e = bpmd_internal_inflate_keyed_split(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap,

@@ -864,7 +864,8 @@ inflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
                const uint32_t* __restrict__ in_len, uint32_t n_msgs, uint8_t* __restrict__ out,
                const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
                uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t raw,
-               const uint32_t* __restrict__ mask_key, uint32_t min_in, uint32_t* __restrict__ qctr)
+               const uint32_t* __restrict__ mask_key, uint32_t min_in, uint32_t* __restrict__ qctr,
+               const uint32_t* __restrict__ order, const uint32_t* __restrict__ limit)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     WaveLds& L = *reinterpret_cast<WaveLds*>(smem);
@@ -891,14 +892,18 @@ inflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
     if (qctr) {
         // work queue: a wave takes the next message when its last one is
         // done, so waves that share a SIMD with more waves (9 per CU on 4
-        // SIMDs) take fewer messages instead of setting the launch's end
+        // SIMDs) take fewer messages instead of setting the launch's end.
+        // order/limit: the messages are order[0, *limit) (the long payloads
+        // of a lane-kernel batch, pmd_capi.hip inflate_impl)
+        const uint32_t end = limit ? *limit : n_msgs;
         for (;;) {
             uint32_t k = 0;
             if (lane_id() == 0) k = atomicAdd(qctr, 1u);
             k = (uint32_t)__builtin_amdgcn_readfirstlane((int)k);
-            if (k >= n_msgs) break;
-            if (min_in && in_len[k] <= min_in) continue;
-            run(k);
+            if (k >= end) break;
+            const uint32_t msg = order ? order[k] : k;
+            if (min_in && in_len[msg] <= min_in) continue;
+            run(msg);
         }
         return;
     }
@@ -947,7 +952,31 @@ extern "C" int bpmd_internal_inflate_keyed_split(const uint8_t* in, const uint64
         if (!qctr || hipMemsetAsync(qctr, 0, sizeof(uint32_t), stream) != hipSuccess) return (int)hipErrorOutOfMemory;
     }
     hipLaunchKernelGGL(inflate_kernel, dim3(grid), dim3(WAVE), lds, stream, in, in_off, in_len, n, out, out_off,
-                       out_cap, out_len, status, raw, mask_key, min_in, qctr);
+                       out_cap, out_len, status, raw, mask_key, min_in, qctr, (const uint32_t*)nullptr,
+                       (const uint32_t*)nullptr);
+    return (int)hipGetLastError();
+}
+
+// The long payloads of a lane-kernel batch: messages order[0, *limit) (a
+// device count, known only on the device), one wave each from the work queue.
+extern "C" int bpmd_internal_inflate_wave_ordered(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                                  uint32_t n, uint8_t* out, const uint64_t* out_off,
+                                                  const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
+                                                  uint32_t raw, const uint32_t* mask_key, const uint32_t* order,
+                                                  const uint32_t* limit, hipStream_t stream)
+{
+    using namespace bpmd;
+    if (n == 0) return 0;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const size_t lds = sizeof(WaveLds);
+    const unsigned per_cu = (unsigned)(160 * 1024 / lds);
+    unsigned grid = (unsigned)cus * (per_cu ? per_cu : 1);
+    if (grid > n) grid = n;
+    uint32_t* qctr = (uint32_t*)bpmd_internal_scratch(stream, 256, 6);
+    if (!qctr || hipMemsetAsync(qctr, 0, sizeof(uint32_t), stream) != hipSuccess) return (int)hipErrorOutOfMemory;
+    hipLaunchKernelGGL(inflate_kernel, dim3(grid), dim3(WAVE), lds, stream, in, in_off, in_len, n, out, out_off,
+                       out_cap, out_len, status, raw, mask_key, 0u, qctr, order, limit);
     return (int)hipGetLastError();
 }
 

@@ -478,7 +478,7 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
                                         const uint32_t* __restrict__ out_cap, uint32_t raw,
                                         const uint32_t* __restrict__ mask_key, const uint32_t* __restrict__ hist_len,
                                         uint32_t hist_max, uint32_t n_msgs, const uint32_t* __restrict__ order,
-                                        uint32_t* __restrict__ qctr)
+                                        uint32_t* __restrict__ qctr, uint32_t s0)
 {
     uint32_t* H = (uint32_t*)(T + O_HIST);
     uint16_t* LE = (uint16_t*)(T + O_LE);
@@ -558,7 +558,7 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
     // that finds the queue empty sends EXIT
     uint32_t msg = m;
     bool send_new = false, send_exit = false, exhausted = qctr == nullptr;
-    const uint32_t first_slots = gridDim.x * WG_MSGS;
+    const uint32_t first_slots = s0 + gridDim.x * WG_MSGS;
     auto begin = [&](uint32_t mm) {
         msg = mm;
         const uint8_t* p = in + in_off[mm];
@@ -1218,14 +1218,18 @@ inflate_lane3_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict_
                      const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
                      uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t raw,
                      const uint32_t* __restrict__ mask_key, const uint32_t* __restrict__ hist_len, uint32_t hist_max,
-                     uint32_t max_in, const uint32_t* __restrict__ order, uint32_t* __restrict__ qctr)
+                     uint32_t max_in, const uint32_t* __restrict__ order, uint32_t* __restrict__ qctr,
+                     const uint32_t* __restrict__ skip)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const unsigned lane = threadIdx.x & 63u;
     const bool is_decoder = threadIdx.x < 64;
     uint8_t* T = smem + lane * STRIDE;
-    // first message: slot blockIdx.x * 64 + lane (of `order` when given)
-    const uint32_t j = blockIdx.x * WG_MSGS + lane;
+    // skip: the first *skip entries of `order` belong to the wave kernel (the
+    // long payloads of a work-queue batch, pmd_capi.hip inflate_impl)
+    const uint32_t s0 = skip ? *skip : 0u;
+    // first message: slot s0 + blockIdx.x * 64 + lane (of `order` when given)
+    const uint32_t j = s0 + blockIdx.x * WG_MSGS + lane;
     bool valid = j < n_msgs;
     const uint32_t m = valid ? (order ? order[j] : j) : 0u;
     // max_in != 0: only payloads of at most max_in bytes (the rest go to the
@@ -1235,7 +1239,7 @@ inflate_lane3_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict_
     __syncthreads();
     if (is_decoder) {
         if (BPMD3_DPRIO) __builtin_amdgcn_s_setprio(BPMD3_DPRIO);   // the decoder sets the pace
-        decoder(T, valid, m, in, in_off, in_len, out_cap, raw, mask_key, hist_len, hist_max, n_msgs, order, qctr);
+        decoder(T, valid, m, in, in_off, in_len, out_cap, raw, mask_key, hist_len, hist_max, n_msgs, order, qctr, s0);
     } else {
         expander(T, valid, m, out, out_off, out_cap, out_len, status, hist_len, hist_max, qctr != nullptr);
     }
@@ -1252,14 +1256,15 @@ extern "C" int bpmd_internal_inflate_lane3(const uint8_t* in, const uint64_t* in
                                            uint32_t* out_len, int32_t* status, uint32_t raw, const uint32_t* mask_key,
                                            const uint32_t* hist_len, uint32_t hist_max, uint32_t max_in,
                                            const uint32_t* order, uint32_t* qctr, uint32_t grid_wgs,
-                                           hipStream_t stream)
+                                           const uint32_t* skip, hipStream_t stream)
 {
     using namespace bpmd::lp3;
     if (n == 0) return 0;
     unsigned grid = (n + WG_MSGS - 1) / WG_MSGS;
     if (qctr && grid_wgs && grid > grid_wgs) grid = grid_wgs;
     hipLaunchKernelGGL(inflate_lane3_kernel, dim3(grid), dim3(128), WG_MSGS * STRIDE, stream, in, in_off, in_len, n,
-                       out, out_off, out_cap, out_len, status, raw, mask_key, hist_len, hist_max, max_in, order, qctr);
+                       out, out_off, out_cap, out_len, status, raw, mask_key, hist_len, hist_max, max_in, order, qctr,
+                       skip);
     return (int)hipGetLastError();
 }
 
@@ -1285,8 +1290,10 @@ __global__ void __launch_bounds__(256) order_keys_kernel(const uint32_t* __restr
 
 extern "C" void* bpmd_internal_scratch(hipStream_t s, size_t bytes, int which);
 
-// order[0, n) = message indices, longest payload first; returns null on error
-extern "C" const uint32_t* bpmd_internal_lane_order(const uint32_t* in_len, uint32_t n, hipStream_t stream)
+// order[0, n) = message indices, longest payload first; returns null on error.
+// keys_out (optional): the sorted keys (in_len >> 6, descending).
+extern "C" const uint32_t* bpmd_internal_lane_order(const uint32_t* in_len, uint32_t n, hipStream_t stream,
+                                                    const uint32_t** keys_out)
 {
     size_t temp = 0;
     if (hipcub::DeviceRadixSort::SortPairsDescending(nullptr, temp, (const uint32_t*)nullptr, (uint32_t*)nullptr,
@@ -1306,7 +1313,62 @@ extern "C" const uint32_t* bpmd_internal_lane_order(const uint32_t* in_len, uint
     if (hipcub::DeviceRadixSort::SortPairsDescending(tmp, temp, kin, kout, iin, iout, (int)n, 0, 26, stream) !=
         hipSuccess)
         return nullptr;
+    if (keys_out) *keys_out = kout;
     return iout;
+}
+
+// ------------------------------------------------------------ long payloads
+// A lane decodes one message serially, so in a work-queue batch a payload
+// that alone takes longer than the whole batch's share per lane sets the
+// launch's end (at 8 GPUs, each rank's C4 shard ran ~20 ms on its 64 KiB
+// messages against ~5 ms for the rest).  Those payloads go to the wave
+// kernel, which decodes one message with 64 lanes.  "Longer than its share":
+// compressed length above 2x the batch's compressed bytes per resident lane,
+// and never below 4 KiB (the per-message split the two kernels were tuned
+// at).  The count is computed on the device from the sorted keys, so the
+// call stays asynchronous: split[0] = total compressed bytes (u64),
+// split[2] = number of long payloads = a prefix of the longest-first order.
+namespace bpmd {
+namespace lp3 {
+__global__ void __launch_bounds__(256) sum_in_kernel(const uint32_t* __restrict__ in_len, uint32_t n,
+                                                     unsigned long long* __restrict__ total)
+{
+    unsigned long long acc = 0;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) acc += in_len[i];
+    for (int d = 32; d >= 1; d >>= 1) acc += __shfl_down(acc, d);
+    if ((threadIdx.x & 63) == 0 && acc) atomicAdd(total, acc);
+}
+__global__ void long_count_kernel(const uint32_t* __restrict__ keys, uint32_t n, uint32_t lanes,
+                                  unsigned long long* __restrict__ split)
+{
+    if (threadIdx.x != 0) return;
+    const unsigned long long total = split[0];
+    unsigned long long thr = 2ull * total / (lanes ? lanes : 1u);
+    if (thr < 4096) thr = 4096;
+    const uint32_t tk = (uint32_t)((thr + 63) >> 6);   // long: key > tk (keys descending)
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (keys[mid] > tk) lo = mid + 1;
+        else hi = mid;
+    }
+    ((uint32_t*)split)[2] = lo;
+}
+}  // namespace lp3
+}  // namespace bpmd
+
+// returns a device pointer to the number of long payloads (a prefix of the
+// order bpmd_internal_lane_order returned with `keys`), or null on error
+extern "C" const uint32_t* bpmd_internal_lane_long_split(const uint32_t* in_len, const uint32_t* keys, uint32_t n,
+                                                         uint32_t lanes, hipStream_t stream)
+{
+    unsigned long long* split = (unsigned long long*)bpmd_internal_scratch(stream, 256, 9);
+    if (!split || hipMemsetAsync(split, 0, 16, stream) != hipSuccess) return nullptr;
+    const uint32_t blocks = n / 256 + 1 < 1024 ? n / 256 + 1 : 1024;
+    hipLaunchKernelGGL(bpmd::lp3::sum_in_kernel, dim3(blocks), dim3(256), 0, stream, in_len, n, split);
+    hipLaunchKernelGGL(bpmd::lp3::long_count_kernel, dim3(1), dim3(64), 0, stream, keys, n, lanes, split);
+    if (hipGetLastError() != hipSuccess) return nullptr;
+    return (const uint32_t*)split + 2;
 }
 
 // diagnostic counters of the pipelined lane kernel (meaningful only in the -DBPMD_PROF build)

@@ -135,3 +135,42 @@ def test_c4_work_queue_batch():
             assert np.array_equal(got, raw[:int(ln.astype(np.int64).sum())])
         finally:
             pmd.lib().bpmd_set_inflate_kernel(0)
+
+
+def test_c4_long_payloads_split_to_wave_kernel():
+    """A work-queue batch whose longest payloads exceed twice the batch's
+    compressed bytes per resident lane (and 4 KiB): those are decoded by the
+    wave kernel from the longest-first order while the lane kernel takes the
+    rest (pmd_capi.hip inflate_impl, bpmd_internal_lane_long_split).  Every
+    message -- including corrupted long and short ones -- must equal the
+    oracle's inflate in status and bytes."""
+    import torch
+    from beast_amd import pmd
+    n = 70000
+    lens = synth.zipf_sizes(n, 0x5EED0045)
+    raw, off, ln = synth.make_batch("json", lens, seed=0x5EED0045)
+    comp, coff, clen, st = O.deflate_batch(raw, off, ln, level=6, mem_level=4, threads=16)
+    assert (st == 0).all()
+    thr = max(4096, 2 * int(clen.astype(np.int64).sum()) // 65536)
+    longs = np.nonzero(clen > thr)[0]
+    assert len(longs) > 20, len(longs)   # the split is exercised
+    comp = comp.copy()
+    rng = np.random.default_rng(45)
+    for i in list(longs[:8]) + list(rng.choice(n, 8, replace=False)):
+        j = int(coff[i]) + int(rng.integers(int(clen[i]) // 2, int(clen[i])))
+        comp[j] ^= 0x10
+    cap = ln.astype(np.uint32)
+    exp_out, exp_off, exp_len, exp_st = O.inflate_batch(comp, coff, clen, cap, threads=16)
+    src = pmd.Batch.from_arrays(comp, coff.astype(np.int64), clen.astype(np.int32))
+    r = pmd.inflate_batch(src, torch.from_numpy(cap.astype(np.int32)).cuda())
+    torch.cuda.synchronize()
+    got_st = r.status.cpu().numpy()
+    got_len = r.out.len.cpu().numpy()
+    assert np.array_equal(got_st, exp_st), np.nonzero(got_st != exp_st)[0][:10]
+    assert np.array_equal(got_len, exp_len.astype(got_len.dtype))
+    outs = r.out.data.cpu().numpy()
+    o_off = r.out.off.cpu().numpy()
+    for i in range(n):
+        a, b = int(o_off[i]), int(exp_off[i])
+        k = int(exp_len[i])
+        assert np.array_equal(outs[a:a + k], exp_out[b:b + k]), i
