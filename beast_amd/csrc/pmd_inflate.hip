@@ -71,7 +71,7 @@ constexpr unsigned SEG_TOKENS = BPMD_SEG_TOKENS;   // target tokens per lane seg
 constexpr unsigned SEG_MAX_BITS = 300;   // keeps a round inside the window
 constexpr unsigned BM_WORDS = (R_MAX + 128) / 32 + 2;
 
-enum Ev : uint32_t { EV_NONE = 0, EV_EOB, EV_ERROR, EV_STARVED, EV_FULL, EV_PARTIAL };
+enum Ev : uint32_t { EV_NONE = 0, EV_EOB, EV_ERROR, EV_STARVED, EV_FULL, EV_PARTIAL, EV_LIMIT };
 
 struct alignas(16) WaveLds {
     uint8_t ring[RING];
@@ -91,6 +91,14 @@ static_assert((WAVE * SEG_MAX_BITS + 160) / 8 + 16 <= IN_CAP, "a round's segment
 
 __device__ uint16_t g_fixed_lens[512];
 __device__ uint16_t g_fixed_dists[32];
+// round mode (bpmd_diag_set_wave_walk, tests): 0 automatic, 1 walk rounds
+// only, 2 speculative rounds only
+__device__ uint32_t g_wave_walk;
+
+// A speculative round whose pass B needed more re-runs than this switches the
+// message to walk rounds: its segments do not re-synchronise (near-random
+// literals with codes of nearly one length, C5), so pass B ran serially.
+constexpr uint32_t WALK_AFTER = 6;
 
 // Diagnostic build only (-DBPMD_PROF): per-phase cycle and event counters.
 __device__ unsigned long long g_prof[24];
@@ -383,6 +391,12 @@ __device__ __forceinline__ uint32_t from_prev_lane(uint32_t x) { return __shfl_u
 
 __device__ __forceinline__ unsigned first_lane(uint64_t mask) { return mask ? (unsigned)__builtin_ctzll(mask) : WAVE; }
 
+// set bits of m below this lane
+__device__ __forceinline__ uint32_t popc_below_lane(uint64_t m)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 // ------------------------------------------------------------------- output
 
 struct Out {
@@ -503,6 +517,8 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
     uint32_t pos = 0;   // stream bit position (wave-uniform)
     bool last = false;
     uint32_t est16 = 8 * 16;   // estimated bits per token, x16
+    const uint32_t wmode = g_wave_walk;
+    bool walk = wmode == 1;
 
     for (;;) {
         unsigned type;
@@ -722,6 +738,98 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
         while (!stop && !block_end) {
             PROF_CNT(6, 1);
             const uint32_t S = pos;
+            if (walk) {
+                // ---- walk round: lane j decodes the token starting at bit
+                // p0 + j; the true chain from p0 is found by pointer doubling
+                // over the 64 candidates, so every step is exact whatever the
+                // code (no re-synchronisation needed) and yields the tokens
+                // starting in [p0, p0 + 64).  The reference's per-token
+                // checks apply to the chain members in order, as in
+                // decode_store; the first member with an event ends the round.
+                for (unsigned i = lane; i < BM_WORDS; i += WAVE) L.u.bitmap[i] = 0;
+                wave_sync();
+                uint32_t p0 = S, ntok = 0, nbyte = 0, wev = EV_NONE, werr = 0;
+                for (;;) {
+                    ensure(p0, 24);
+                    const uint32_t wbw = wbase * 8;
+                    const uint32_t p = p0 + lane;
+                    const uint64_t v = peek64(L.win, p - wbw);
+                    const uint32_t avail = p < total_bits ? total_bits - p : 0;
+                    const Tok t = decode_tok(v, avail, T.ltab, T.lroot, T.dtab, T.droot);
+                    uint32_t J = t.ev == EV_NONE ? lane + t.nbits : (uint32_t)WAVE;   // an event ends the chain
+                    uint64_t R = (1ull << lane) | (J < WAVE ? (1ull << J) : 0ull);
+#pragma unroll
+                    for (int k = 0; k < 6; ++k) {
+                        const uint32_t jj = J < WAVE ? J : lane;
+                        const uint32_t rlo = __shfl((uint32_t)R, jj), rhi = __shfl((uint32_t)(R >> 32), jj);
+                        const uint32_t j2 = __shfl(J, jj);
+                        const uint64_t keep = J < WAVE ? ~0ull : 0ull;
+                        R |= (((uint64_t)rhi << 32) | rlo) & keep;
+                        J = J < WAVE ? j2 : J;
+                    }
+                    const uint64_t M = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(R >> 32)) << 32) |
+                                       (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)R);
+                    const bool mem = (M >> lane) & 1;
+                    const uint32_t idx = popc_below_lane(M);   // order of this member in the chain
+                    const uint32_t ol = mem && t.ev == EV_NONE ? t.olen : 0u;
+                    const uint32_t ol_incl = scan_incl(ol);
+                    const uint32_t abs = o.pos + nbyte + ol_incl - ol;
+                    const bool is_match = t.olen > 1 || (t.info >> 16) != 0;
+                    // the member's event, in decode_store's order; EV_LIMIT:
+                    // the round's token list or ring is full before it
+                    uint32_t e = EV_NONE;
+                    if (mem) {
+                        if (t.ev != EV_NONE) e = t.ev;
+                        else if (ntok + idx >= TOT || nbyte + ol_incl > R_MAX) e = EV_LIMIT;
+                        else if (raw && abs >= o.cap) e = EV_FULL;
+                        else if (is_match && (t.info & 0xffffu) > abs) e = EV_ERROR;
+                        else if (abs >= o.cap) e = EV_FULL;
+                        else if (abs + t.olen > o.cap) e = EV_PARTIAL;
+                    }
+                    const uint64_t em = __ballot(e != EV_NONE);
+                    const unsigned fe = first_lane(em);
+                    // members before the first event are stored; a partial one too
+                    const bool store = mem && (lane < fe || (lane == fe && e == EV_PARTIAL));
+                    if (store) {
+                        L.tok[ntok + idx] = t.info;
+                        const uint32_t rel = abs - o.pos;
+                        atomicOr(&L.u.bitmap[rel >> 5], 1u << (rel & 31));
+                    }
+                    const uint64_t sm = __ballot(store);
+                    const unsigned nst = (unsigned)__builtin_popcountll(sm);
+                    if (fe == WAVE) {   // the whole window's chain is in: next window
+                        const unsigned last = 63u - (unsigned)__builtin_clzll(M);
+                        ntok += nst;
+                        nbyte = __shfl(nbyte + ol_incl, last);
+                        p0 = p0 + last + __shfl(t.nbits, last);
+                        continue;
+                    }
+                    const uint32_t ee = __shfl(e, fe);
+                    const uint32_t before = __shfl(nbyte + ol_incl - ol, fe);   // bytes of the members before
+                    ntok += nst;
+                    if (ee == EV_PARTIAL) {
+                        nbyte = before + (o.cap - __shfl(abs, fe));
+                        p0 = p0 + fe + __shfl(t.nbits, fe);
+                    } else {
+                        nbyte = before;
+                        p0 = p0 + fe + (ee == EV_EOB ? __shfl(t.nbits, fe) : 0u);
+                    }
+                    wev = ee == EV_LIMIT ? (uint32_t)EV_NONE : ee;
+                    // (a decode error, or a distance past the output so far)
+                    werr = __shfl(t.ev == EV_ERROR ? t.err : (uint32_t)ST_INVALID_DISTANCE, fe);
+                    break;
+                }
+                wave_sync();
+                expand_round(L, o, nbyte);
+                switch (wev) {
+                case EV_NONE: pos = p0; break;
+                case EV_EOB: pos = p0; block_end = true; break;
+                case EV_ERROR: st = (int32_t)werr; stop = true; break;
+                case EV_STARVED: pos = p0; stop = true; break;
+                default: st = full_status; pos = p0; stop = true; break;
+                }
+                continue;
+            }
             const uint32_t rem = total_bits > S ? total_bits - S : 0;
             // segments keep ~SEG_TOKENS tokens even when the block is short:
             // shorter ones would rarely re-synchronise; lanes past the end of
@@ -756,8 +864,10 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
             }
 #endif
             unsigned k;   // last lane of the round
+            uint32_t reruns = 0;
             for (;;) {
                 PROF_CNT(7, 1);
+                ++reruns;
                 const uint32_t prev_exit = from_prev_lane(b.exit);
                 const bool bad = lane > 0 && start != prev_exit;
                 const uint64_t evm = __ballot(b.ev != EV_NONE);
@@ -825,6 +935,7 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
             if (round_toks) est16 = ((kexit - S) << 4) / round_toks;
             if (est16 < 16) est16 = 16;
             shrink = 0;
+            if (wmode == 0 && reruns > WALK_AFTER) walk = true;
             switch (kev) {
             case EV_NONE:
                 pos = kexit;
@@ -1016,6 +1127,16 @@ extern "C" int bpmd_internal_init_fixed(void)
     if (e != hipSuccess) return (int)e;
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_fixed_dists), fd, sizeof fd);
     return (int)e;
+}
+
+// round mode of the wave kernel (tests, A/B): 0 automatic, 1 walk rounds only,
+// 2 speculative rounds only
+extern "C" int bpmd_diag_set_wave_walk(int mode)
+{
+    using namespace bpmd;
+    if (mode < 0 || mode > 2) return -1;
+    const uint32_t v = (uint32_t)mode;
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_wave_walk), &v, sizeof v);
 }
 
 // diagnostic counters (meaningful only in the -DBPMD_PROF build)

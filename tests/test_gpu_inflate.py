@@ -14,15 +14,20 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 
-@pytest.fixture(autouse=True, params=["lane", "wave"])
+@pytest.fixture(autouse=True, params=["lane", "wave", "wave_walk", "wave_spec"])
 def inflate_kernel(request):
-    """Every inflate test runs on both kernels (pmd_inflate_lane.hip and
-    pmd_inflate.hip), forced through bpmd_set_inflate_kernel."""
+    """Every inflate test runs on both kernels (pmd_inflate_lane3.hip and
+    pmd_inflate.hip), forced through bpmd_set_inflate_kernel; the wave kernel
+    also with every round a walk round and with speculative rounds only
+    (bpmd_diag_set_wave_walk)."""
     pmd = _pmd()
-    mode = {"lane": 1, "wave": 2}[request.param]
+    mode = {"lane": 1, "wave": 2, "wave_walk": 2, "wave_spec": 2}[request.param]
+    walk = {"wave_walk": 1, "wave_spec": 2}.get(request.param, 0)
     assert pmd.lib().bpmd_set_inflate_kernel(mode) == 0
+    assert pmd.lib().bpmd_diag_set_wave_walk(walk) == 0
     yield request.param
     pmd.lib().bpmd_set_inflate_kernel(0)
+    pmd.lib().bpmd_diag_set_wave_walk(0)
 
 
 def _pmd():
