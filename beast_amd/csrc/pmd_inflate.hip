@@ -37,6 +37,7 @@
 #include "pmd_common.h"
 #include "huff_table.h"
 #include "huff_wave.h"
+#include "wave_util.h"
 
 namespace bpmd {
 
@@ -99,6 +100,7 @@ __device__ uint32_t g_wave_walk;
 // message to walk rounds: its segments do not re-synchronise (near-random
 // literals with codes of nearly one length, C5), so pass B ran serially.
 constexpr uint32_t WALK_AFTER = 6;
+constexpr int WQ = 4;   // walk window: 64 x WQ candidate bit offsets
 
 // Diagnostic build only (-DBPMD_PROF): per-phase cycle and event counters.
 __device__ unsigned long long g_prof[24];
@@ -195,7 +197,6 @@ __device__ __forceinline__ uint32_t gbyte(const uint8_t* p)
     return (v >> ((a & 3) * 8)) & 0xffu;
 }
 
-__device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); asm volatile("" ::: "memory"); }
 
 // ------------------------------------------------------------- token decode
 
@@ -739,84 +740,107 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
             PROF_CNT(6, 1);
             const uint32_t S = pos;
             if (walk) {
-                // ---- walk round: lane j decodes the token starting at bit
-                // p0 + j; the true chain from p0 is found by pointer doubling
-                // over the 64 candidates, so every step is exact whatever the
-                // code (no re-synchronisation needed) and yields the tokens
-                // starting in [p0, p0 + 64).  The reference's per-token
-                // checks apply to the chain members in order, as in
-                // decode_store; the first member with an event ends the round.
+                // ---- walk round: lane j decodes the tokens starting at bits
+                // p0 + j + 64q (q < WQ); the true chain from p0 is then
+                // followed on the scalar unit through those candidates
+                // (v_readlane of their lengths), so every step is exact
+                // whatever the code -- no re-synchronisation needed -- and
+                // yields the tokens starting in [p0, p0 + 64 WQ).  The
+                // reference's per-token checks apply to the chain members in
+                // order, as in decode_store; the first member with an event
+                // ends the round.
                 for (unsigned i = lane; i < BM_WORDS; i += WAVE) L.u.bitmap[i] = 0;
                 wave_sync();
                 uint32_t p0 = S, ntok = 0, nbyte = 0, wev = EV_NONE, werr = 0;
                 for (;;) {
-                    ensure(p0, 24);
+                    ensure(p0, 8 * WQ + 16);
                     const uint32_t wbw = wbase * 8;
-                    const uint32_t p = p0 + lane;
-                    const uint64_t v = peek64(L.win, p - wbw);
-                    const uint32_t avail = p < total_bits ? total_bits - p : 0;
-                    const Tok t = decode_tok(v, avail, T.ltab, T.lroot, T.dtab, T.droot);
-                    uint32_t J = t.ev == EV_NONE ? lane + t.nbits : (uint32_t)WAVE;   // an event ends the chain
-                    uint64_t R = (1ull << lane) | (J < WAVE ? (1ull << J) : 0ull);
+                    Tok t[WQ];
+                    uint32_t nbq[WQ];
 #pragma unroll
-                    for (int k = 0; k < 6; ++k) {
-                        const uint32_t jj = J < WAVE ? J : lane;
-                        const uint32_t rlo = __shfl((uint32_t)R, jj), rhi = __shfl((uint32_t)(R >> 32), jj);
-                        const uint32_t j2 = __shfl(J, jj);
-                        const uint64_t keep = J < WAVE ? ~0ull : 0ull;
-                        R |= (((uint64_t)rhi << 32) | rlo) & keep;
-                        J = J < WAVE ? j2 : J;
+                    for (int q = 0; q < WQ; ++q) {
+                        const uint32_t p = p0 + 64u * q + lane;
+                        const uint32_t avail = p < total_bits ? total_bits - p : 0;
+                        t[q] = decode_tok(peek64(L.win, p - wbw), avail, T.ltab, T.lroot, T.dtab, T.droot);
+                        nbq[q] = t[q].ev == EV_NONE ? t[q].nbits : 0u;   // 0: an event ends the chain
                     }
-                    const uint64_t M = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(R >> 32)) << 32) |
-                                       (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)R);
-                    const bool mem = (M >> lane) & 1;
-                    const uint32_t idx = popc_below_lane(M);   // order of this member in the chain
-                    const uint32_t ol = mem && t.ev == EV_NONE ? t.olen : 0u;
-                    const uint32_t ol_incl = scan_incl(ol);
-                    const uint32_t abs = o.pos + nbyte + ol_incl - ol;
-                    const bool is_match = t.olen > 1 || (t.info >> 16) != 0;
-                    // the member's event, in decode_store's order; EV_LIMIT:
-                    // the round's token list or ring is full before it
-                    uint32_t e = EV_NONE;
-                    if (mem) {
-                        if (t.ev != EV_NONE) e = t.ev;
-                        else if (ntok + idx >= TOT || nbyte + ol_incl > R_MAX) e = EV_LIMIT;
-                        else if (raw && abs >= o.cap) e = EV_FULL;
-                        else if (is_match && (t.info & 0xffffu) > abs) e = EV_ERROR;
-                        else if (abs >= o.cap) e = EV_FULL;
-                        else if (abs + t.olen > o.cap) e = EV_PARTIAL;
+                    // the chain, on scalar registers
+                    uint64_t M[WQ];
+                    uint32_t cur = 0;
+                    bool ended = false;
+#pragma unroll
+                    for (int q = 0; q < WQ; ++q) {
+                        M[q] = 0;
+                        while (!ended && cur < 64u * (q + 1)) {
+                            const uint32_t l = cur - 64u * q;
+                            M[q] |= 1ull << l;
+                            const uint32_t nb = (uint32_t)__builtin_amdgcn_readlane((int)nbq[q], (int)l);
+                            if (nb == 0) ended = true;
+                            else cur += nb;
+                        }
                     }
-                    const uint64_t em = __ballot(e != EV_NONE);
-                    const unsigned fe = first_lane(em);
-                    // members before the first event are stored; a partial one too
-                    const bool store = mem && (lane < fe || (lane == fe && e == EV_PARTIAL));
-                    if (store) {
-                        L.tok[ntok + idx] = t.info;
-                        const uint32_t rel = abs - o.pos;
-                        atomicOr(&L.u.bitmap[rel >> 5], 1u << (rel & 31));
+                    // members in chain order: output offsets, events, stores
+                    uint32_t base_tok = 0, base_byte = 0, fe = 64u * WQ, fev = EV_NONE;
+                    uint32_t fe_before = 0, fe_abs = 0, fe_nb = 0, fe_err = 0;
+#pragma unroll
+                    for (int q = 0; q < WQ; ++q) {
+                        const bool mem = (M[q] >> lane) & 1;
+                        const uint32_t idx = base_tok + popc_below_lane(M[q]);
+                        const uint32_t ol = mem && t[q].ev == EV_NONE ? t[q].olen : 0u;
+                        const uint32_t ol_incl = base_byte + wave_scan_incl(ol);
+                        const uint32_t abs = o.pos + nbyte + ol_incl - ol;
+                        const bool is_match = t[q].olen > 1 || (t[q].info >> 16) != 0;
+                        uint32_t e = EV_NONE;
+                        if (mem && fe == 64u * WQ) {
+                            if (t[q].ev != EV_NONE) e = t[q].ev;
+                            else if (ntok + idx >= TOT || nbyte + ol_incl > R_MAX) e = EV_LIMIT;
+                            else if (raw && abs >= o.cap) e = EV_FULL;
+                            else if (is_match && (t[q].info & 0xffffu) > abs) e = EV_ERROR;
+                            else if (abs >= o.cap) e = EV_FULL;
+                            else if (abs + t[q].olen > o.cap) e = EV_PARTIAL;
+                        }
+                        const unsigned f = first_lane(__ballot(e != EV_NONE));
+                        const bool store = mem && fe == 64u * WQ && (lane < f || (lane == f && e == EV_PARTIAL));
+                        if (store) {
+                            L.tok[ntok + idx] = t[q].info;
+                            const uint32_t rel = abs - o.pos;
+                            atomicOr(&L.u.bitmap[rel >> 5], 1u << (rel & 31));
+                        }
+                        if (fe == 64u * WQ && f < WAVE) {
+                            fe = 64u * q + f;
+                            fev = (uint32_t)__builtin_amdgcn_readlane((int)e, (int)f);
+                            fe_before = (uint32_t)__builtin_amdgcn_readlane((int)(ol_incl - ol), (int)f);
+                            fe_abs = (uint32_t)__builtin_amdgcn_readlane((int)abs, (int)f);
+                            fe_nb = (uint32_t)__builtin_amdgcn_readlane((int)t[q].nbits, (int)f);
+                            fe_err = (uint32_t)__builtin_amdgcn_readlane(
+                                (int)(t[q].ev == EV_ERROR ? t[q].err : (uint32_t)ST_INVALID_DISTANCE), (int)f);
+                        }
+                        base_tok += (uint32_t)__builtin_popcountll(M[q]);
+                        base_byte = (uint32_t)__builtin_amdgcn_readlane((int)ol_incl, 63);
                     }
-                    const uint64_t sm = __ballot(store);
-                    const unsigned nst = (unsigned)__builtin_popcountll(sm);
-                    if (fe == WAVE) {   // the whole window's chain is in: next window
-                        const unsigned last = 63u - (unsigned)__builtin_clzll(M);
-                        ntok += nst;
-                        nbyte = __shfl(nbyte + ol_incl, last);
-                        p0 = p0 + last + __shfl(t.nbits, last);
+                    if (fe == 64u * WQ) {   // the window's whole chain is in: the next window
+                        ntok += base_tok;
+                        nbyte += base_byte;
+                        p0 += cur;
                         continue;
                     }
-                    const uint32_t ee = __shfl(e, fe);
-                    const uint32_t before = __shfl(nbyte + ol_incl - ol, fe);   // bytes of the members before
-                    ntok += nst;
-                    if (ee == EV_PARTIAL) {
-                        nbyte = before + (o.cap - __shfl(abs, fe));
-                        p0 = p0 + fe + __shfl(t.nbits, fe);
-                    } else {
-                        nbyte = before;
-                        p0 = p0 + fe + (ee == EV_EOB ? __shfl(t.nbits, fe) : 0u);
+                    ntok += (uint32_t)__builtin_popcountll(M[0] & ((fe >= 64 ? ~0ull : ((1ull << fe) - 1ull))));
+#pragma unroll
+                    for (int q = 1; q < WQ; ++q) {
+                        const uint32_t lo = 64u * q;
+                        const uint64_t below = fe <= lo ? 0ull : fe >= lo + 64 ? ~0ull : ((1ull << (fe - lo)) - 1ull);
+                        ntok += (uint32_t)__builtin_popcountll(M[q] & below);
                     }
-                    wev = ee == EV_LIMIT ? (uint32_t)EV_NONE : ee;
-                    // (a decode error, or a distance past the output so far)
-                    werr = __shfl(t.ev == EV_ERROR ? t.err : (uint32_t)ST_INVALID_DISTANCE, fe);
+                    if (fev == EV_PARTIAL) {
+                        ntok += 1;
+                        nbyte += fe_before + (o.cap - fe_abs);
+                        p0 += fe + fe_nb;
+                    } else {
+                        nbyte += fe_before;
+                        p0 += fe + (fev == EV_EOB ? fe_nb : 0u);
+                    }
+                    wev = fev == EV_LIMIT ? (uint32_t)EV_NONE : fev;
+                    werr = fev == EV_ERROR ? fe_err : 0u;
                     break;
                 }
                 wave_sync();
