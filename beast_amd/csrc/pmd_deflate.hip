@@ -1507,6 +1507,19 @@ extern "C" int bpmd_internal_deflate_bits(const uint8_t* in, const uint64_t* in_
                         level, window_bits, strategy, stream, tune);
 }
 
+// the per-stream deflater's flush (pmd_stream.hip): exact bit lengths, and
+// the stream's earlier plaintext before the message as history (context
+// takeover), hist_len null for none
+extern "C" int bpmd_internal_deflate_bits_hist(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                               uint32_t n, uint8_t* out, const uint64_t* out_off,
+                                               const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
+                                               uint32_t* out_bits, const uint32_t* hist_len, int level,
+                                               int window_bits, int strategy, const int* tune, hipStream_t stream)
+{
+    return deflate_impl(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, out_bits, nullptr, hist_len,
+                        level, window_bits, strategy, stream, tune);
+}
+
 extern "C" int bpmd_internal_deflate_keyed(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                            uint32_t n, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                                            uint32_t* out_len, int32_t* status, int level, int window_bits,

@@ -28,15 +28,17 @@
 #include <vector>
 
 #include "../../include/beast_pmd.h"
+#include "lz_core.h"
 #include "zstream.h"
 
 extern "C" int bpmd_internal_zstream_write(void* st, const uint8_t* in, uint64_t n_in, uint8_t* out, uint64_t cap,
                                            int flush, void* res, hipStream_t stream);
 extern "C" void bpmd_internal_scratch_release(hipStream_t stream);
-extern "C" int bpmd_internal_deflate_bits(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
-                                          uint32_t n, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
-                                          uint32_t* out_len, int32_t* status, uint32_t* out_bits, int level,
-                                          int window_bits, int strategy, const int* tune, hipStream_t stream);
+extern "C" int bpmd_internal_deflate_bits_hist(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                               uint32_t n, uint8_t* out, const uint64_t* out_off,
+                                               const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
+                                               uint32_t* out_bits, const uint32_t* hist_len, int level,
+                                               int window_bits, int strategy, const int* tune, hipStream_t stream);
 
 struct bpmd_stream {
     bool is_deflate = true;
@@ -50,8 +52,12 @@ struct bpmd_stream {
     size_t din_cap = 0;
     uint8_t* dout = nullptr;
     size_t dout_cap = 0;
-    // deflate: buffered message bytes
+    // deflate: buffered message bytes; the plaintext already compressed since
+    // the last reset (its last BPMD_CHUNK_HIST bytes: the history the next
+    // flush's matches may reach into, as Beast's window does across flushes
+    // and, under context takeover, across messages)
     std::vector<uint8_t> in;
+    std::vector<uint8_t> hist;
     // deflate: output not yet handed out, plus < 8 pending bits
     std::vector<uint8_t> pend;
     size_t pend_pos = 0;
@@ -92,33 +98,38 @@ struct Meta {
     uint64_t in_off, out_off;
     uint32_t in_len, out_cap, out_len, bits;
     int32_t status;
-    uint32_t pad[6];
+    uint32_t hist_len;
+    uint32_t pad[5];
 };
 static_assert(sizeof(Meta) == 64, "meta block");
 
-// one message through a batch kernel; returns 0 or a negative bpmd_result
-int run_one(bpmd_stream* s, bool deflate, const uint8_t* in, size_t n, size_t out_cap, std::vector<uint8_t>& out,
-            int32_t& status, uint32_t& bits)
+// one flush's bytes through the deflate kernels with the stream's history in
+// front of them; returns 0 or a negative bpmd_result
+int run_one(bpmd_stream* s, const uint8_t* in, size_t n, size_t out_cap, std::vector<uint8_t>& out, int32_t& status,
+            uint32_t& bits)
 {
-    if (n > 0xFFFFFFFFu || out_cap > 0xFFFFFFFFu) return BPMD_R_INVALID_ARGUMENT;
+    const size_t hn = s->hist.size();
+    if (n + hn > 0xFFFFFFFFu || out_cap > 0xFFFFFFFFu) return BPMD_R_INVALID_ARGUMENT;
     int r = bpmd_init();
     if (r) return r;
-    const size_t in_at = 64, out_at = (in_at + n + 15) & ~size_t(15);
+    const size_t in_at = 64, out_at = (in_at + hn + n + 15) & ~size_t(15);
     if ((r = ensure_device(s, out_at + out_cap + 16)) != 0) return r;
     Meta m{};
-    m.in_off = 0;
+    m.in_off = hn;
     m.out_off = 0;
     m.in_len = (uint32_t)n;
     m.out_cap = (uint32_t)out_cap;
+    m.hist_len = (uint32_t)hn;
     uint8_t* d = s->dmem;
     if (hipMemcpyAsync(d, &m, sizeof m, hipMemcpyHostToDevice, s->hs) != hipSuccess) return BPMD_R_HIP_ERROR;
-    if (n && hipMemcpyAsync(d + in_at, in, n, hipMemcpyHostToDevice, s->hs) != hipSuccess) return BPMD_R_HIP_ERROR;
+    if (hn && hipMemcpyAsync(d + in_at, s->hist.data(), hn, hipMemcpyHostToDevice, s->hs) != hipSuccess)
+        return BPMD_R_HIP_ERROR;
+    if (n && hipMemcpyAsync(d + in_at + hn, in, n, hipMemcpyHostToDevice, s->hs) != hipSuccess) return BPMD_R_HIP_ERROR;
     Meta* dm = (Meta*)d;
-    int e;
-    (void)deflate;
-    e = bpmd_internal_deflate_bits(d + in_at, &dm->in_off, &dm->in_len, 1, d + out_at, &dm->out_off, &dm->out_cap,
-                                   &dm->out_len, &dm->status, &dm->bits, s->level, s->wbits, s->strategy,
-                                   s->tuned ? s->tune4 : nullptr, s->hs);
+    const int e = bpmd_internal_deflate_bits_hist(d + in_at, &dm->in_off, &dm->in_len, 1, d + out_at, &dm->out_off,
+                                                  &dm->out_cap, &dm->out_len, &dm->status, &dm->bits,
+                                                  hn ? &dm->hist_len : nullptr, s->level, s->wbits, s->strategy,
+                                                  s->tuned ? s->tune4 : nullptr, s->hs);
     if (e) return BPMD_R_HIP_ERROR;
     if (hipMemcpyAsync(&m, d, sizeof m, hipMemcpyDeviceToHost, s->hs) != hipSuccess) return BPMD_R_HIP_ERROR;
     if (hipStreamSynchronize(s->hs) != hipSuccess) return BPMD_R_HIP_ERROR;
@@ -128,6 +139,18 @@ int run_one(bpmd_stream* s, bool deflate, const uint8_t* in, size_t n, size_t ou
     status = m.status;
     bits = m.bits;
     return BPMD_R_OK;
+}
+
+// the flushed bytes become history; only the last BPMD_CHUNK_HIST are used
+void add_history(bpmd_stream* s, const uint8_t* p, size_t n)
+{
+    constexpr size_t keep = BPMD_CHUNK_HIST;
+    if (n >= keep) {
+        s->hist.assign(p + n - keep, p + n);
+        return;
+    }
+    s->hist.insert(s->hist.end(), p, p + n);
+    if (s->hist.size() > keep) s->hist.erase(s->hist.begin(), s->hist.end() - (ptrdiff_t)keep);
 }
 
 // ------------------------------------------------------------ deflate bits
@@ -183,6 +206,7 @@ bool has_pending(const bpmd_stream* s) { return s->pend_pos < s->pend.size(); }
 void reset_deflate(bpmd_stream* s)
 {
     s->in.clear();
+    s->hist.clear();
     s->pend.clear();
     s->pend_pos = 0;
     s->bits = 0;
@@ -257,10 +281,11 @@ extern "C" int bpmd_deflate_stream_write(bpmd_stream* s, bpmd_zparams* zs, int f
             int32_t st = 0;
             uint32_t nb = 0;
             const size_t cap = bpmd_deflate_upper_bound(s->in.size()) + 16;
-            int r = run_one(s, true, s->in.data(), s->in.size(), cap, out, st, nb);
+            int r = run_one(s, s->in.data(), s->in.size(), cap, out, st, nb);
             if (r) return r;
             if (st != BPMD_OK) return BPMD_STREAM_ERROR;
             put_bitstring(s, out.data(), nb);
+            add_history(s, s->in.data(), s->in.size());
             s->in.clear();
         }
         switch (flush) {

@@ -176,3 +176,39 @@ def test_inflate_errors_reported():
     zs = ZParams(ctypes.addressof(src), 1, 0, ctypes.cast(out, ctypes.c_void_p), 16, 0, 2)
     assert O.ERRORS[L.bpmd_inflate_stream_write(zi, ctypes.byref(zs), SYNC)] == "invalid_block_type"
     L.bpmd_stream_destroy(zi)
+
+
+# Σ GPU payload bytes / Σ Beast payload bytes for a connection's messages
+# under context takeover (the deflater is never reset): the GPU's matches
+# reach at most BPMD_CHUNK_HIST bytes into earlier messages, Beast's the
+# whole window.  Measured and stated here.
+TAKEOVER_TOLERANCE = 1.35
+
+
+def test_context_takeover_per_stream_sizes_and_roundtrip():
+    """configs[0]'s shape, 1 Ki x 1 KiB text messages on one connection with
+    the default context takeover (compLevel 8, memLevel 4, option.hpp:61-64):
+    the per-stream deflater keeps its history across messages as Beast's
+    does; every payload inflates through one never-reset inflater (the
+    oracle's and the GPU's), and the total size is within
+    TAKEOVER_TOLERANCE of Beast's own payloads."""
+    L = _lib()
+    zo = ctypes.c_void_p()
+    assert L.bpmd_deflate_stream_create(8, 15, 4, 0, ctypes.byref(zo)) == 0
+    zi = _mk(L, False)
+    data, off, lens = synth.make_batch("json", [1024] * 1024, seed=0x5EED0001)
+    msgs = [bytes(data[int(off[i]):int(off[i]) + 1024]) for i in range(1024)]
+    try:
+        pays = [ws_deflate_message(L, zo, m) for m in msgs]
+        for i, p in enumerate(pays[:64]):
+            assert ws_inflate_message(L, zi, p) == msgs[i], i
+    finally:
+        L.bpmd_stream_destroy(zo)
+        L.bpmd_stream_destroy(zi)
+    back = O.pmd_inflate_stream(pays, cap=4096)
+    assert all(b == (0, m) for b, m in zip(back, msgs))
+    beast = O.pmd_deflate_stream(msgs, 8, 15, 4)
+    ratio = sum(map(len, pays)) / sum(map(len, beast))
+    no_hist = sum(len(O.pmd_deflate(m, 8, 15, 4)) for m in msgs) / sum(map(len, beast))
+    print(f"takeover per-stream size / Beast = {ratio:.4f} (without cross-message history: {no_hist:.4f})")
+    assert ratio <= TAKEOVER_TOLERANCE, ratio
