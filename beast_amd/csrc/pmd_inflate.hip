@@ -92,14 +92,15 @@ static_assert((WAVE * SEG_MAX_BITS + 160) / 8 + 16 <= IN_CAP, "a round's segment
 
 __device__ uint16_t g_fixed_lens[512];
 __device__ uint16_t g_fixed_dists[32];
-// round mode (bpmd_diag_set_wave_walk, tests): 0 automatic, 1 walk rounds
-// only, 2 speculative rounds only
+// round mode (bpmd_diag_set_wave_walk, tests and A/B): 0 automatic (fixed
+// blocks decoded serially on the scalar unit, the rest in speculative
+// rounds), 1 walk rounds for every block, 2 speculative rounds for every block.
+// Walk rounds (lane j decodes the token at bit p0 + j, the chain followed
+// through the candidates) are exact without re-synchronisation but measured
+// slower than speculative rounds on every corpus tried (C5: 28.5 vs 38.3 GiB/s),
+// so they are not chosen automatically.
 __device__ uint32_t g_wave_walk;
 
-// A speculative round whose pass B needed more re-runs than this switches the
-// message to walk rounds: its segments do not re-synchronise (near-random
-// literals with codes of nearly one length, C5), so pass B ran serially.
-constexpr uint32_t WALK_AFTER = 6;
 constexpr int WQ = 4;   // walk window: 64 x WQ candidate bit offsets
 
 // Diagnostic build only (-DBPMD_PROF): per-phase cycle and event counters.
@@ -731,6 +732,106 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
             break;
         }
 
+        // ---- a fixed-Huffman block, decoded serially on the scalar unit
+        // straight into the ring.  The fixed code is known in closed form
+        // (RFC 1951 3.2.6), so a symbol costs a few scalar instructions and
+        // no table lookup; speculative rounds gain nothing here because
+        // literals of near-random data (8- and 9-bit codes) do not
+        // re-synchronise (C5's payloads: ~35 % of their tokens are in fixed
+        // blocks).  The reference's fill rule and checks are those of
+        // decode_tok / decode_store: 9 bits before a literal/length code,
+        // then its extra bits, 5 more before the distance code, then its
+        // extra bits (inflate_stream.ipp:360-474); raw-mode full buffer,
+        // distance, capacity (ipp:475-514).
+        if (type == 1 && wmode == 0) {
+            uint64_t bb = 0;          // bit buffer: the bn stream bits from bit `pos` on
+            uint32_t bn = 0;
+            uint32_t since = 1u << 30;   // literals since the last ring_reserve
+            auto refill = [&]() {
+                while (bn < 32) {
+                    const uint32_t nb = pos + bn;              // next stream bit to buffer
+                    ensure(nb & ~31u, 8);
+                    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane(
+                        (int)L.win[(((nb & ~31u) >> 3) - wbase) >> 2]);
+                    const uint32_t sh = nb & 31u;              // only the first word can start inside
+                    bb |= (uint64_t)(w >> sh) << bn;
+                    bn += 32 - sh;
+                }
+            };
+            bool stop = false;
+            for (;;) {
+                refill();
+                const uint32_t avail = total_bits > pos ? total_bits - pos : 0u;
+                if (avail < 9) { stop = true; break; }   // starved: the slow path asks for lenbits_ = 9
+                const uint32_t c9 = __builtin_bitreverse32((uint32_t)bb & 0x1ffu) >> 23;
+                uint32_t sym, used;
+                if ((c9 >> 2) < 24) { sym = 256 + (c9 >> 2); used = 7; }
+                else if ((c9 >> 1) >= 0x30 && (c9 >> 1) < 0xc0) { sym = (c9 >> 1) - 0x30; used = 8; }
+                else if ((c9 >> 1) >= 0xc0 && (c9 >> 1) < 0xc8) { sym = 280 + (c9 >> 1) - 0xc0; used = 8; }
+                else { sym = 144 + c9 - 0x190; used = 9; }
+                const uint32_t abs = o.pos;
+                if (sym < 256) {
+                    if (abs >= o.cap) { st = full_status; stop = true; break; }
+                    if (since >= 256) {
+                        ring_reserve(L, o, 512);
+                        since = 0;
+                    }
+                    if (lane == 0) L.ring[abs & RING_MASK] = (uint8_t)sym;
+                    o.pos = abs + 1;
+                    ++since;
+                    bb >>= used;
+                    bn -= used;
+                    pos += used;
+                    continue;
+                }
+                if (sym == 256) {   // end of block
+                    bb >>= used;
+                    bn -= used;
+                    pos += used;
+                    break;
+                }
+                if (sym > 285) { st = ST_INVALID_LITERAL_LENGTH; stop = true; break; }
+                const uint32_t li = sym - 257;
+                const uint32_t xl = kLenExtra[li];
+                const uint32_t len = kLenBase[li] + ((uint32_t)(bb >> used) & ((1u << xl) - 1u));
+                used += xl;
+                if (avail < used || avail < used + 5) { stop = true; break; }   // starved
+                const uint32_t d5 = __builtin_bitreverse32((uint32_t)(bb >> used) & 31u) >> 27;
+                if (d5 >= 30) { st = ST_INVALID_DISTANCE_CODE; stop = true; break; }
+                const uint32_t xd = kDistExtra[d5];
+                const uint32_t dist = kDistBase[d5] + ((uint32_t)(bb >> (used + 5)) & ((1u << xd) - 1u));
+                used += 5 + xd;
+                if (avail < used) { stop = true; break; }   // starved
+                if (raw && abs >= o.cap) { st = full_status; stop = true; break; }
+                if (dist > abs) { st = ST_INVALID_DISTANCE; stop = true; break; }
+                if (abs >= o.cap) { st = full_status; stop = true; break; }
+                const bool partial = abs + len > o.cap;
+                const uint32_t n = partial ? o.cap - abs : len;
+                ring_reserve(L, o, 258);
+                wave_sync();
+                for (uint32_t j0 = 0; j0 < n; j0 += WAVE) {
+                    const uint32_t j = j0 + lane;
+                    if (j < n) {
+                        const uint32_t k = dist >= n ? j : j % dist;
+                        const uint32_t src = abs - dist + k;
+                        // a source within the ring has not been overwritten
+                        // yet (dist <= RING); older ones are flushed
+                        const uint32_t val = dist <= RING ? (uint32_t)L.ring[src & RING_MASK] : gbyte(o.g + src);
+                        L.ring[(abs + j) & RING_MASK] = (uint8_t)val;
+                    }
+                }
+                wave_sync();
+                o.pos = abs + n;
+                bb >>= used;
+                bn -= used;
+                pos += used;
+                if (partial) { st = full_status; stop = true; break; }
+            }
+            wave_sync();
+            if (stop) break;
+            continue;
+        }
+
         // ---- compressed data, in rounds (ipp:356-514)
         PROF_LAP(1);
         PROF_CNT(8, 1);
@@ -959,7 +1060,7 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
             if (round_toks) est16 = ((kexit - S) << 4) / round_toks;
             if (est16 < 16) est16 = 16;
             shrink = 0;
-            if (wmode == 0 && reruns > WALK_AFTER) walk = true;
+            (void)reruns;
             switch (kev) {
             case EV_NONE:
                 pos = kexit;
