@@ -746,7 +746,7 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
         if (type == 1 && wmode == 0) {
             uint64_t bb = 0;          // bit buffer: the bn stream bits from bit `pos` on
             uint32_t bn = 0;
-            uint32_t since = 1u << 30;   // literals since the last ring_reserve
+            uint32_t rlim = 0;   // ring positions below rlim may be written (ring_reserve)
             auto refill = [&]() {
                 while (bn < 32) {
                     const uint32_t nb = pos + bn;              // next stream bit to buffer
@@ -772,13 +772,12 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
                 const uint32_t abs = o.pos;
                 if (sym < 256) {
                     if (abs >= o.cap) { st = full_status; stop = true; break; }
-                    if (since >= 256) {
+                    if (abs >= rlim) {
                         ring_reserve(L, o, 512);
-                        since = 0;
+                        rlim = abs + 512;
                     }
                     if (lane == 0) L.ring[abs & RING_MASK] = (uint8_t)sym;
                     o.pos = abs + 1;
-                    ++since;
                     bb >>= used;
                     bn -= used;
                     pos += used;
@@ -807,7 +806,10 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
                 if (abs >= o.cap) { st = full_status; stop = true; break; }
                 const bool partial = abs + len > o.cap;
                 const uint32_t n = partial ? o.cap - abs : len;
-                ring_reserve(L, o, 258);
+                if (abs + 258 > rlim) {
+                    ring_reserve(L, o, 512);
+                    rlim = abs + 512;
+                }
                 wave_sync();
                 for (uint32_t j0 = 0; j0 < n; j0 += WAVE) {
                     const uint32_t j = j0 + lane;
@@ -815,7 +817,8 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
                         const uint32_t k = dist >= n ? j : j % dist;
                         const uint32_t src = abs - dist + k;
                         // a source within the ring has not been overwritten
-                        // yet (dist <= RING); older ones are flushed
+                        // yet (dist <= RING); older ones are flushed (the
+                        // reserve covers abs + 258 - RING)
                         const uint32_t val = dist <= RING ? (uint32_t)L.ring[src & RING_MASK] : gbyte(o.g + src);
                         L.ring[(abs + j) & RING_MASK] = (uint8_t)val;
                     }
