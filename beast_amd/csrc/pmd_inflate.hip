@@ -92,16 +92,21 @@ static_assert((WAVE * SEG_MAX_BITS + 160) / 8 + 16 <= IN_CAP, "a round's segment
 
 __device__ uint16_t g_fixed_lens[512];
 __device__ uint16_t g_fixed_dists[32];
-// round mode (bpmd_diag_set_wave_walk, tests and A/B): 0 automatic (fixed
-// blocks decoded serially on the scalar unit, the rest in speculative
-// rounds), 1 walk rounds for every block, 2 speculative rounds for every block.
-// Walk rounds (lane j decodes the token at bit p0 + j, the chain followed
-// through the candidates) are exact without re-synchronisation but measured
-// slower than speculative rounds on every corpus tried (C5: 28.5 vs 38.3 GiB/s),
-// so they are not chosen automatically.
+// round mode (bpmd_diag_set_wave_walk, tests and A/B): 0 automatic, 1 walk
+// rounds for every block, 2 speculative rounds for every block.  Walk rounds
+// (lane j decodes the token at bit p0 + j + 64q, the chain followed through
+// the candidates on the scalar unit) are exact without re-synchronisation;
+// which mode is faster depends on the data (scripts/diag_wave_rate.py:
+// Beast's own 64 KiB binary payloads, mostly fixed blocks of near-random
+// literals, 21.2 vs 10.6 GiB/s for walk; JSON 38.6 vs 53.7 for speculative),
+// so the automatic mode measures both on each message (s_memtime per round)
+// and keeps the one with fewer cycles per token: a speculative round whose
+// pass B needed more than WALK_PROBE re-runs is followed by a walk round, and
+// every 16 rounds the mode not in use is measured again.
 __device__ uint32_t g_wave_walk;
 
 constexpr int WQ = 4;   // walk window: 64 x WQ candidate bit offsets
+constexpr uint32_t WALK_PROBE = 4;
 
 // Diagnostic build only (-DBPMD_PROF): per-phase cycle and event counters.
 __device__ unsigned long long g_prof[24];
@@ -519,8 +524,12 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
     uint32_t pos = 0;   // stream bit position (wave-uniform)
     bool last = false;
     uint32_t est16 = 8 * 16;   // estimated bits per token, x16
+    // round mode (g_wave_walk): forced, or chosen per message by the cycles
+    // per token each mode measured on this message's recent rounds
     const uint32_t wmode = g_wave_walk;
     bool walk = wmode == 1;
+    uint32_t cpt_spec = 0, cpt_walk = 0;   // cycles per token x16 of the last round of each mode (0: unknown)
+    uint32_t rounds = 0;
 
     for (;;) {
         unsigned type;
@@ -732,109 +741,6 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
             break;
         }
 
-        // ---- a fixed-Huffman block, decoded serially on the scalar unit
-        // straight into the ring.  The fixed code is known in closed form
-        // (RFC 1951 3.2.6), so a symbol costs a few scalar instructions and
-        // no table lookup; speculative rounds gain nothing here because
-        // literals of near-random data (8- and 9-bit codes) do not
-        // re-synchronise (C5's payloads: ~35 % of their tokens are in fixed
-        // blocks).  The reference's fill rule and checks are those of
-        // decode_tok / decode_store: 9 bits before a literal/length code,
-        // then its extra bits, 5 more before the distance code, then its
-        // extra bits (inflate_stream.ipp:360-474); raw-mode full buffer,
-        // distance, capacity (ipp:475-514).
-        if (type == 1 && wmode == 0) {
-            uint64_t bb = 0;          // bit buffer: the bn stream bits from bit `pos` on
-            uint32_t bn = 0;
-            uint32_t rlim = 0;   // ring positions below rlim may be written (ring_reserve)
-            auto refill = [&]() {
-                while (bn < 32) {
-                    const uint32_t nb = pos + bn;              // next stream bit to buffer
-                    ensure(nb & ~31u, 8);
-                    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane(
-                        (int)L.win[(((nb & ~31u) >> 3) - wbase) >> 2]);
-                    const uint32_t sh = nb & 31u;              // only the first word can start inside
-                    bb |= (uint64_t)(w >> sh) << bn;
-                    bn += 32 - sh;
-                }
-            };
-            bool stop = false;
-            for (;;) {
-                refill();
-                const uint32_t avail = total_bits > pos ? total_bits - pos : 0u;
-                if (avail < 9) { stop = true; break; }   // starved: the slow path asks for lenbits_ = 9
-                const uint32_t c9 = __builtin_bitreverse32((uint32_t)bb & 0x1ffu) >> 23;
-                uint32_t sym, used;
-                if ((c9 >> 2) < 24) { sym = 256 + (c9 >> 2); used = 7; }
-                else if ((c9 >> 1) >= 0x30 && (c9 >> 1) < 0xc0) { sym = (c9 >> 1) - 0x30; used = 8; }
-                else if ((c9 >> 1) >= 0xc0 && (c9 >> 1) < 0xc8) { sym = 280 + (c9 >> 1) - 0xc0; used = 8; }
-                else { sym = 144 + c9 - 0x190; used = 9; }
-                const uint32_t abs = o.pos;
-                if (sym < 256) {
-                    if (abs >= o.cap) { st = full_status; stop = true; break; }
-                    if (abs >= rlim) {
-                        ring_reserve(L, o, 512);
-                        rlim = abs + 512;
-                    }
-                    if (lane == 0) L.ring[abs & RING_MASK] = (uint8_t)sym;
-                    o.pos = abs + 1;
-                    bb >>= used;
-                    bn -= used;
-                    pos += used;
-                    continue;
-                }
-                if (sym == 256) {   // end of block
-                    bb >>= used;
-                    bn -= used;
-                    pos += used;
-                    break;
-                }
-                if (sym > 285) { st = ST_INVALID_LITERAL_LENGTH; stop = true; break; }
-                const uint32_t li = sym - 257;
-                const uint32_t xl = kLenExtra[li];
-                const uint32_t len = kLenBase[li] + ((uint32_t)(bb >> used) & ((1u << xl) - 1u));
-                used += xl;
-                if (avail < used || avail < used + 5) { stop = true; break; }   // starved
-                const uint32_t d5 = __builtin_bitreverse32((uint32_t)(bb >> used) & 31u) >> 27;
-                if (d5 >= 30) { st = ST_INVALID_DISTANCE_CODE; stop = true; break; }
-                const uint32_t xd = kDistExtra[d5];
-                const uint32_t dist = kDistBase[d5] + ((uint32_t)(bb >> (used + 5)) & ((1u << xd) - 1u));
-                used += 5 + xd;
-                if (avail < used) { stop = true; break; }   // starved
-                if (raw && abs >= o.cap) { st = full_status; stop = true; break; }
-                if (dist > abs) { st = ST_INVALID_DISTANCE; stop = true; break; }
-                if (abs >= o.cap) { st = full_status; stop = true; break; }
-                const bool partial = abs + len > o.cap;
-                const uint32_t n = partial ? o.cap - abs : len;
-                if (abs + 258 > rlim) {
-                    ring_reserve(L, o, 512);
-                    rlim = abs + 512;
-                }
-                wave_sync();
-                for (uint32_t j0 = 0; j0 < n; j0 += WAVE) {
-                    const uint32_t j = j0 + lane;
-                    if (j < n) {
-                        const uint32_t k = dist >= n ? j : j % dist;
-                        const uint32_t src = abs - dist + k;
-                        // a source within the ring has not been overwritten
-                        // yet (dist <= RING); older ones are flushed (the
-                        // reserve covers abs + 258 - RING)
-                        const uint32_t val = dist <= RING ? (uint32_t)L.ring[src & RING_MASK] : gbyte(o.g + src);
-                        L.ring[(abs + j) & RING_MASK] = (uint8_t)val;
-                    }
-                }
-                wave_sync();
-                o.pos = abs + n;
-                bb >>= used;
-                bn -= used;
-                pos += used;
-                if (partial) { st = full_status; stop = true; break; }
-            }
-            wave_sync();
-            if (stop) break;
-            continue;
-        }
-
         // ---- compressed data, in rounds (ipp:356-514)
         PROF_LAP(1);
         PROF_CNT(8, 1);
@@ -843,6 +749,10 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
         while (!stop && !block_end) {
             PROF_CNT(6, 1);
             const uint32_t S = pos;
+            const uint64_t t_round = wmode == 0 ? __builtin_amdgcn_s_memtime() : 0ull;
+            // every 16 rounds one round runs in the mode not in use, so its
+            // measure stays current (the data may change character)
+            if (wmode == 0 && (++rounds & 15) == 0 && cpt_spec && cpt_walk) walk = !walk;
             if (walk) {
                 // ---- walk round: lane j decodes the tokens starting at bits
                 // p0 + j + 64q (q < WQ); the true chain from p0 is then
@@ -949,6 +859,10 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
                 }
                 wave_sync();
                 expand_round(L, o, nbyte);
+                if (wmode == 0 && ntok >= 64) {
+                    cpt_walk = (uint32_t)(((__builtin_amdgcn_s_memtime() - t_round) << 4) / ntok);
+                    walk = !(cpt_spec && cpt_spec < cpt_walk);
+                }
                 switch (wev) {
                 case EV_NONE: pos = p0; break;
                 case EV_EOB: pos = p0; block_end = true; break;
@@ -1063,7 +977,12 @@ __device__ void inflate_msg(WaveLds& L, const Msg& m, Out& o, bool raw, uint32_t
             if (round_toks) est16 = ((kexit - S) << 4) / round_toks;
             if (est16 < 16) est16 = 16;
             shrink = 0;
-            (void)reruns;
+            if (wmode == 0 && round_toks >= 64) {
+                cpt_spec = (uint32_t)(((__builtin_amdgcn_s_memtime() - t_round) << 4) / round_toks);
+                // pass B ran (nearly) serially: measure a walk round, unless
+                // one was measured slower
+                walk = cpt_walk ? cpt_walk < cpt_spec : reruns > WALK_PROBE;
+            }
             switch (kev) {
             case EV_NONE:
                 pos = kexit;

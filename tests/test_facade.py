@@ -52,6 +52,33 @@ def test_impl_base_codec_uses_compile():
     assert r.returncode == 0, r.stderr
 
 
+def _build_cpu_echo():
+    """ws_echo.cpp linked against tests/cpp/oracle_backend.c (Beast's zlib
+    restated, CPU) instead of libbeast_pmd.so: the same C1 harness, timed
+    the same way, with the reference's CPU codec (test infrastructure)."""
+    os.makedirs(BUILD, exist_ok=True)
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "liboracle.so"], check=True)
+    odir = os.path.join(ROOT, "oracle")
+    lib = os.path.join(BUILD, "libbpmd_oracle_backend.so")
+    out = os.path.join(BUILD, "ws_echo_cpu")
+    subprocess.run(["gcc", "-O2", "-fPIC", "-shared", "-o", lib, os.path.join(CPP, "oracle_backend.c"),
+                    "-L", odir, "-loracle", f"-Wl,-rpath,{odir}"], check=True)
+    subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(CPP, "ws_echo.cpp"), "-o", out, "-L", BUILD, "-lbpmd_oracle_backend",
+                    f"-Wl,-rpath,{BUILD}", "-lpthread"], check=True)
+    return out
+
+
+def test_c1_loopback_echo_cpu_oracle():
+    """configs[0] ("Beast CPU zlib only"): the C1 echo with Beast's own codec
+    (its C restatement) on the CPU, the number the GPU facade's echo time is
+    compared with."""
+    r = subprocess.run([_build_cpu_echo(), "1024", "1024"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "echo ok: 1024 messages x 1024 B" in r.stdout, r.stdout
+    print(r.stdout)
+
+
 def test_without_gpu_engine_reports_instead_of_falling_back():
     import torch
     if torch.cuda.is_available():
@@ -67,13 +94,29 @@ def test_facade_roundtrip_on_gpu():
     assert r.stdout.count("ok") == 4
 
 
+def _wire(out):
+    import re
+    m = re.search(r"wire (\d+) B client->server, (\d+) B server->client, ([0-9.]+) s", out)
+    return int(m.group(1)), int(m.group(2)), float(m.group(3))
+
+
 @pytest.mark.gpu
 def test_c1_loopback_echo_on_gpu():
-    """configs[0]: 1 Ki x 1 KiB text messages echoed over loopback."""
+    """configs[0]: 1 Ki x 1 KiB text messages echoed over loopback through the
+    GPU facade, next to the same harness on Beast's CPU codec: the echo is
+    exact, and the wire bytes (the payloads, context takeover on) stay
+    within tests/test_gpu_stream.py's TAKEOVER_TOLERANCE of Beast's."""
+    from tests.test_gpu_stream import TAKEOVER_TOLERANCE
     r = subprocess.run([_build("ws_echo"), "1024", "1024"], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "echo ok: 1024 messages x 1024 B" in r.stdout, r.stdout
-    print(r.stdout)
+    c = subprocess.run([_build_cpu_echo(), "1024", "1024"], capture_output=True, text=True, timeout=300)
+    assert c.returncode == 0, c.stdout + c.stderr
+    g1, g2, gt = _wire(r.stdout)
+    b1, b2, bt = _wire(c.stdout)
+    print(f"C1 echo: GPU facade {gt:.3f} s, Beast CPU codec {bt:.3f} s; wire bytes GPU/Beast "
+          f"{(g1 + g2) / (b1 + b2):.4f}")
+    assert (g1 + g2) <= TAKEOVER_TOLERANCE * (b1 + b2)
 
 
 def test_msg_size_threshold_decisions():
