@@ -34,6 +34,7 @@ def _lib():
     L.bpmd_deflate_stream_reset.argtypes = [vp]
     L.bpmd_inflate_stream_reset.argtypes = [vp, ctypes.c_int]
     L.bpmd_stream_destroy.argtypes = [vp]
+    L.bpmd_internal_scratch_count.restype = ctypes.c_size_t
     return L
 
 
@@ -212,3 +213,29 @@ def test_context_takeover_per_stream_sizes_and_roundtrip():
     no_hist = sum(len(O.pmd_deflate(m, 8, 15, 4)) for m in msgs) / sum(map(len, beast))
     print(f"takeover per-stream size / Beast = {ratio:.4f} (without cross-message history: {no_hist:.4f})")
     assert ratio <= TAKEOVER_TOLERANCE, ratio
+
+
+def test_stream_churn_releases_device_scratch():
+    """Per-stream codecs own a HIP stream and the scratch blocks the batch
+    kernels allocate for it; destroying the codec releases them
+    (bpmd_internal_scratch_release), so connection churn does not grow device
+    memory or the scratch table."""
+    L = _lib()
+    L.bpmd_internal_scratch_count.restype = ctypes.c_size_t
+    d, _, _ = synth.make_batch("json", [9000], seed=8)
+    msg = bytes(d[:9000])
+
+    def one():
+        zo, zi = _mk(L, True), _mk(L, False)
+        try:
+            p = ws_deflate_message(L, zo, msg)
+            assert ws_inflate_message(L, zi, p) == msg
+        finally:
+            L.bpmd_stream_destroy(zo)
+            L.bpmd_stream_destroy(zi)
+
+    one()
+    base = L.bpmd_internal_scratch_count()
+    for _ in range(100):
+        one()
+    assert L.bpmd_internal_scratch_count() == base
