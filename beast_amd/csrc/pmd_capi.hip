@@ -31,7 +31,11 @@ extern "C" int bpmd_internal_inflate_lane3(const uint8_t* in, const uint64_t* in
 extern "C" const uint32_t* bpmd_internal_lane_order(const uint32_t* in_len, uint32_t n, hipStream_t stream,
                                                     const uint32_t** keys_out);
 extern "C" const uint32_t* bpmd_internal_lane_long_split(const uint32_t* in_len, const uint32_t* keys, uint32_t n,
-                                                         uint32_t lanes, hipStream_t stream);
+                                                         uint32_t lanes, uint32_t min_thr, hipStream_t stream);
+extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n,
+                                        uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                                        uint32_t* out_len, int32_t* status, uint32_t raw, const uint32_t* order,
+                                        const uint32_t* nlong, hipStream_t s);
 extern "C" int bpmd_internal_inflate_wave_ordered(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                                   uint32_t n, uint8_t* out, const uint64_t* out_off,
                                                   const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
@@ -139,7 +143,8 @@ uint8_t* scratch_for(hipStream_t s, size_t bytes, int which = 0)
 
 // scratch block `which` (0 inflate queue, 1-2 deflate workspace, 3-4 exact
 // deflate queue and workspace, 5 inflate message order, 6 wave inflate queue,
-// 7 deflate chunk queue, 8 multi-device output totals, 9 long-payload split)
+// 7 deflate chunk queue, 8 multi-device output totals, 9 long-payload split,
+// 10-11 block-parallel inflate stats and decode workspace)
 // for other translation units
 extern "C" void* bpmd_internal_scratch(hipStream_t s, size_t bytes, int which)
 {
@@ -188,13 +193,16 @@ extern "C" void bpmd_diag_set_grid(unsigned grid) { bpmd_diag_grid_override = gr
 
 // Kernel choice for a batch: one lane per message (pmd_inflate_lane3.hip)
 // for throughput, one wave per message (pmd_inflate.hip) for latency when
-// the batch is too small to fill the chip's lanes.  BPMD_INFLATE=lane|wave
-// or bpmd_set_inflate_kernel() forces one (the tests run both).
-static std::atomic<int> g_inflate_kernel{-1};   // -1 unset, 0 auto, 1 lane, 2 wave
+// the batch is too small to fill the chip's lanes, and block-parallel decode
+// (pmd_inflate_bp.hip) for the long payloads of large batches.
+// BPMD_INFLATE=lane|wave|bp or bpmd_set_inflate_kernel() forces one (the
+// tests run all three; "bp" sends every payload of 64 bytes or more through
+// the block-parallel path).
+static std::atomic<int> g_inflate_kernel{-1};   // -1 unset, 0 auto, 1 lane, 2 wave, 3 bp
 
 extern "C" int bpmd_set_inflate_kernel(int mode)
 {
-    if (mode < 0 || mode > 2) return BPMD_R_INVALID_ARGUMENT;
+    if (mode < 0 || mode > 3) return BPMD_R_INVALID_ARGUMENT;
     g_inflate_kernel.store(mode);
     return BPMD_R_OK;
 }
@@ -204,10 +212,20 @@ static int inflate_mode()
     int m = g_inflate_kernel.load();
     if (m < 0) {
         const char* e = getenv("BPMD_INFLATE");
-        m = (e && !strcmp(e, "lane")) ? 1 : (e && !strcmp(e, "wave")) ? 2 : 0;
+        m = (e && !strcmp(e, "lane")) ? 1 : (e && !strcmp(e, "wave")) ? 2 : (e && !strcmp(e, "bp")) ? 3 : 0;
         g_inflate_kernel.store(m);
     }
     return m;
+}
+
+// block-parallel decode of long payloads in automatic mode (BPMD_INFLATE_BP=0: off)
+static bool inflate_bp_enabled()
+{
+    static const bool on = [] {
+        const char* e = getenv("BPMD_INFLATE_BP");
+        return !(e && e[0] == '0');
+    }();
+    return on;
 }
 
 // Automatic choice, per message: a lane-kernel wave lasts as long as its
@@ -263,6 +281,22 @@ int inflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
     if (!mu) return BPMD_R_HIP_ERROR;
     std::lock_guard<std::mutex> launch(*mu);
     const int m = inflate_mode();
+    // block-parallel decode applies to plain batches (no takeover window, no
+    // masking key: the segment decoder starts mid-payload)
+    const bool bp_ok = !hist && !key && ((m == 0 && inflate_bp_enabled()) || m == 3);
+    if (m == 3 && bp_ok) {
+        // forced (tests): every payload of 64 bytes or more, the rest on lanes
+        const uint32_t* keys = nullptr;
+        const uint32_t* order = bpmd_internal_lane_order(d_in_len, n_msgs, s, &keys);
+        const uint32_t* nlong = order ? bpmd_internal_lane_long_split(d_in_len, keys, n_msgs, 0u, 64u, s) : nullptr;
+        if (!nlong || bpmd_internal_inflate_bp(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap,
+                                               d_out_len, d_status, raw, order, nlong, s) ||
+            bpmd_internal_inflate_lane3(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
+                                        d_status, raw, nullptr, nullptr, 1u << cfg->window_bits, 0u, order, nullptr,
+                                        0u, nlong, s))
+            return BPMD_R_HIP_ERROR;
+        return BPMD_R_OK;
+    }
     // lane-kernel share: everything (hist / forced lane), nothing (forced wave /
     // small batch), or the payloads of at most `split` bytes
     const bool lane = hist || m == 1 || (m == 0 && n_msgs >= 2048);
@@ -304,11 +338,28 @@ int inflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
             const uint32_t* keys = nullptr;
             if (ordered && !(order = bpmd_internal_lane_order(d_in_len, n_msgs, s, &keys))) return BPMD_R_HIP_ERROR;
             if (ordered && long_split && m == 0 && !hist) {
-                if (!(nlong = bpmd_internal_lane_long_split(d_in_len, keys, n_msgs, wgs * 64u, s)) ||
-                    bpmd_internal_inflate_wave_ordered(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap,
-                                                       d_out_len, d_status, raw, key, order, nlong, s))
+                // long payloads: block-parallel, or one wave each
+                if (!(nlong = bpmd_internal_lane_long_split(d_in_len, keys, n_msgs, wgs * 64u, 4096u, s)) ||
+                    (bp_ok ? bpmd_internal_inflate_bp(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap,
+                                                      d_out_len, d_status, raw, order, nlong, s)
+                           : bpmd_internal_inflate_wave_ordered(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off,
+                                                                d_out_cap, d_out_len, d_status, raw, key, order,
+                                                                nlong, s)))
                     return BPMD_R_HIP_ERROR;
             }
+        } else if (split && bp_ok) {
+            // payloads over the split: block-parallel; the rest on lanes, in
+            // the same longest-first order after them
+            const uint32_t* keys = nullptr;
+            if (!(order = bpmd_internal_lane_order(d_in_len, n_msgs, s, &keys)) ||
+                !(nlong = bpmd_internal_lane_long_split(d_in_len, keys, n_msgs, 0u, split, s)) ||
+                bpmd_internal_inflate_bp(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
+                                         d_status, raw, order, nlong, s))
+                return BPMD_R_HIP_ERROR;
+            e = bpmd_internal_inflate_lane3(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
+                                            d_status, raw, key, hist, 1u << cfg->window_bits, 0u, order, nullptr, wgs,
+                                            nlong, s);
+            return e ? BPMD_R_HIP_ERROR : BPMD_R_OK;
         }
         e = bpmd_internal_inflate_lane3(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
                                         d_status, raw, key, hist, 1u << cfg->window_bits, split, order, qctr, wgs,

@@ -41,6 +41,8 @@
 #include <hipcub/hipcub.hpp>
 
 #include "pmd_common.h"
+#include "canon.h"
+#include "bp.h"
 
 namespace bpmd {
 namespace lp3 {
@@ -65,6 +67,7 @@ constexpr unsigned WG_MSGS = 64;
 constexpr uint32_t TOK_END = 0x80000000u;   // word 0: out_len, bits 0-7: status
 constexpr uint32_t TOK_NEW = 0x40000000u;   // word 0: the message the lane starts (work queue)
 constexpr uint32_t TOK_EXIT = 0x20000000u;  // the queue is empty: the lane is done
+constexpr uint32_t TOK_STORED = 0x10000000u;  // segment mode: bits 0-15 stored bytes, word 0 their payload offset
 
 #ifndef BPMD3_KLIT
 #define BPMD3_KLIT 4
@@ -101,90 +104,6 @@ __device__ __forceinline__ void lds_store(uint8_t* p, uint32_t v)
     __hip_atomic_store((uint32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
-
-template <int NB>
-struct Canon {
-    uint32_t Q[NB];
-    uint32_t root;   // the reference's (clamped) root table bits
-};
-
-template <int NB>
-__device__ __forceinline__ uint32_t canon_min(const uint32_t (&Q)[NB], uint32_t c)
-{
-    const uint32_t k1 = (c + 1) << 15;
-    uint32_t m = Q[0] - k1;
-#pragma unroll
-    for (int i = 1; i + 1 < NB; i += 2) {
-        const uint32_t x = Q[i] - k1, y = Q[i + 1] - k1;
-        m = __builtin_elementwise_min(m, __builtin_elementwise_min(x, y));
-    }
-    if (NB % 2 == 0) m = __builtin_elementwise_min(m, Q[NB - 1] - k1);
-    return m;
-}
-
-struct Sym {
-    uint32_t L;     // code length
-    uint32_t idx;   // canonical index (0 when invalid)
-    bool inval;
-};
-
-template <int NB>
-__device__ __forceinline__ Sym canon_decode(const uint32_t (&Q)[NB], uint32_t c)
-{
-    const uint32_t m = canon_min<NB>(Q, c);
-    Sym r;
-    r.inval = (m >> 31) != 0;
-    const uint32_t q = m + ((c + 1) << 15);
-    r.L = (q >> 11) & 15u;
-    const int32_t below = (int32_t)(c - (q >> 15)) >> (NB - (int32_t)r.L);   // in [-count_L, -1]
-    r.idx = r.inval ? 0u : (uint32_t)((int32_t)(q & 0x7ffu) + below);
-    return r;
-}
-
-// The reference's slow path asks for the root bits, or for root + sub-table
-// index bits when the code is longer than the root: a sub-table covers one
-// root prefix and is as deep as the longest code under it, i.e. the length
-// of the last code of the prefix's range (inflate_stream.ipp:360-420, 688-709).
-template <int NB>
-__device__ __forceinline__ uint32_t canon_need(const Canon<NB>& t, const Sym& y, uint32_t c)
-{
-    if (y.inval || y.L <= t.root) return t.root;
-    const uint32_t re = c | ((1u << (NB - t.root)) - 1u);
-    return ((canon_min<NB>(t.Q, re) + ((re + 1) << 15)) >> 11) & 15u;
-}
-
-__device__ __forceinline__ uint32_t rev15(uint64_t bb) { return __builtin_bitreverse32((uint32_t)bb) >> 17; }
-__device__ __forceinline__ uint32_t lowmask(uint32_t n) { return n >= 32 ? ~0u : ((1u << n) - 1u); }
-
-// counts c[1..NB] -> canonical words; returns 0, 14 or 15 following
-// inflate_table's acceptance rules (inflate_stream.ipp:574-617).
-// type: 0 codes, 1 lens, 2 dists.  (The first canonical index of length l
-// is the running sum of c[1..l-1]; callers that need it recompute it.)
-template <int NB>
-__device__ __forceinline__ int make_canon(const uint32_t (&c)[16], uint32_t R, int type, Canon<NB>& t)
-{
-    uint32_t lim = 0, cu = 0, nz = 0;   // nz: bit l set when some code has length l
-#pragma unroll
-    for (int l = 1; l <= NB; ++l) {
-        cu += c[l];
-        lim += c[l] << (NB - l);
-        t.Q[l - 1] = (lim << 15) | ((uint32_t)l << 11) | cu;
-        nz |= c[l] ? 1u << l : 0u;
-    }
-    if (nz == 0) {   // empty code: a 1-bit root of invalid slots
-        t.root = 1;
-        return 0;
-    }
-    const uint32_t lo = (uint32_t)__builtin_ctz(nz), hi = 31u - (uint32_t)__builtin_clz(nz);
-    const uint32_t r = R < hi ? R : hi;
-    t.root = r < lo ? lo : r;
-    // The reference's running `left` (2^l minus the codes of length <= l)
-    // ends at 2^NB - lim; a prefix can only be over-subscribed if the whole
-    // Kraft sum is, since the partial sums only grow.
-    if (lim > (1u << NB)) return ST_OVER_SUBSCRIBED_LENGTH;
-    if (lim < (1u << NB) && (type == 0 || hi != 1)) return ST_INCOMPLETE_LENGTH_SET;
-    return 0;
-}
 
 // Input blocks: 16 stream bytes at A + 16*bi, where the payload is
 // [s, s+n) (A = payload & ~3).  issue_block() reads only dwords holding at
@@ -472,18 +391,291 @@ __device__ __forceinline__ void expander(uint8_t* T, bool valid, uint32_t m, uin
     L3_FLUSH(4);
 }
 
+// --------------------------------------------------------- segment expander
+// Segment mode (bp.h): the slot holds 16-bit symbols.  Match sources before
+// the slot's start become references (SYM_REF | k: the byte k + 1 positions
+// before the segment), so a chunk that straddles the start is loaded from
+// the guard or the preceding slot and its early elements replaced; a chunk
+// wholly before the start is not loaded at all.  Same pipeline as
+// expander(): a chunk loaded in one memory section is stored in the next,
+// stores go in output order, spare elements past a token are overwritten
+// by later output, nothing is stored past the slot's capacity.
+typedef uint2 uint2_s __attribute__((aligned(2)));
+typedef uint4 uint4_s __attribute__((aligned(2)));
+
+__device__ __forceinline__ uint32_t ref_pair(uint32_t w, int32_t a)   // elements a, a + 1 packed in w
+{
+    const uint32_t lo = a < 0 ? (bp::SYM_REF | (uint32_t)(-a - 1)) : (w & 0xffffu);
+    const uint32_t hi = a + 1 < 0 ? (bp::SYM_REF | (uint32_t)(-a - 2)) : (w >> 16);
+    return lo | (hi << 16);
+}
+__device__ __forceinline__ uint4 ref_fix(uint4 w, int32_t src)
+{
+    return make_uint4(ref_pair(w.x, src), ref_pair(w.y, src + 2), ref_pair(w.z, src + 4), ref_pair(w.w, src + 6));
+}
+// the 8 symbols before a match of distance p < 8, repeated with period p
+__device__ __forceinline__ uint4 sym_pattern(uint4 w, uint32_t p)
+{
+    const uint32_t e[8] = {w.x & 0xffffu, w.x >> 16, w.y & 0xffffu, w.y >> 16,
+                           w.z & 0xffffu, w.z >> 16, w.w & 0xffffu, w.w >> 16};
+    uint32_t r[8];
+    uint32_t idx = 8 - p;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        uint32_t v = e[0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) v = idx == (uint32_t)k ? e[k] : v;
+        r[j] = v;
+        idx = idx + 1 == 8 ? 8 - p : idx + 1;
+    }
+    return make_uint4(r[0] | (r[1] << 16), r[2] | (r[3] << 16), r[4] | (r[5] << 16), r[6] | (r[7] << 16));
+}
+__device__ __forceinline__ void store_syms8(uint16_t* o, uint32_t dst, uint32_t lim, uint4 w)
+{
+    if (dst + 8 <= lim) {
+        *(uint4_s*)(o + dst) = w;
+        return;
+    }
+    const uint32_t d[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j)
+        if (dst + j < lim) o[dst + j] = (uint16_t)(d[j >> 1] >> (16 * (j & 1)));
+}
+
+// four payload bytes as four symbols (two dwords)
+__device__ __forceinline__ uint32_t sym_lo(uint32_t d) { return __builtin_amdgcn_perm(0u, d, 0x0c010c00u); }
+__device__ __forceinline__ uint32_t sym_hi(uint32_t d) { return __builtin_amdgcn_perm(0u, d, 0x0c030c02u); }
+
+__device__ __forceinline__ void expander_seg(uint8_t* T, bool valid, uint32_t m, uint16_t* __restrict__ sym,
+                                             const bp::SegTask* __restrict__ tasks, bp::SegRes* __restrict__ res,
+                                             bool queue, const uint8_t* __restrict__ in,
+                                             const uint64_t* __restrict__ in_off, const uint32_t* __restrict__ in_len)
+{
+    uint16_t* o = sym;
+    uint32_t cap = 0;
+    const uint8_t* pl = in;   // the task's payload, [pl, pl_end)
+    const uint8_t* pl_end = in;
+    auto slot = [&](uint32_t t) {
+        const bp::SegTask tk = tasks[t];
+        o = sym + tk.sym_off;
+        cap = tk.sym_cap;
+        const uint32_t mm = tk.kind == bp::KIND_NONE ? 0u : tk.msg;
+        pl = in + in_off[mm];
+        pl_end = pl + in_len[mm];
+    };
+    if (valid) slot(m);
+    bool done = !valid;
+    bool exited = !queue && done;
+    uint32_t tail = 0, pos = 0;
+    uint32_t crem = 0, cdist = 0, cq = 0;
+    uint4 cpat = make_uint4(0, 0, 0, 0);
+    uint32_t cpat_st = 0;   // dist < 8: 0 pattern not requested, 1 source in flight, 2 pattern ready
+    bool cst = false, cst_pat = false;
+    uint32_t cdst = 0, csz = 0, cpd = 1;
+    int32_t csrc = 0;
+    uint4 cw = make_uint4(0, 0, 0, 0), cw2 = cw;
+    uint32_t bcnt = 0, bdst = 0, bval = 0;
+    // stored block: bytes left, next source, next symbol; a loaded piece
+    // (up to 32 bytes) is stored in the next memory section
+    uint32_t srem = 0, sdst = 0, sp_dst = 0;
+    const uint8_t* ssrc = in;
+    bool sp = false;
+    uint4 sw0 = make_uint4(0, 0, 0, 0), sw1 = sw0;
+    for (;;) {
+        const bool alive = !exited || crem != 0 || cst || bcnt != 0 || srem != 0 || sp;
+        if (!__ballot(alive)) break;
+        bool worked = cst || bcnt != 0 || crem != 0 || srem != 0 || sp;
+        // ================================================ memory section
+        if (sp) {
+            store_syms8(o, sp_dst, cap, make_uint4(sym_lo(sw0.x), sym_hi(sw0.x), sym_lo(sw0.y), sym_hi(sw0.y)));
+            store_syms8(o, sp_dst + 8, cap, make_uint4(sym_lo(sw0.z), sym_hi(sw0.z), sym_lo(sw0.w), sym_hi(sw0.w)));
+            store_syms8(o, sp_dst + 16, cap, make_uint4(sym_lo(sw1.x), sym_hi(sw1.x), sym_lo(sw1.y), sym_hi(sw1.y)));
+            store_syms8(o, sp_dst + 24, cap, make_uint4(sym_lo(sw1.z), sym_hi(sw1.z), sym_lo(sw1.w), sym_hi(sw1.w)));
+            sp = false;
+        }
+        if (srem) {
+            const uint32_t k = srem < 32 ? srem : 32u;
+            if (ssrc + 32 <= pl_end) {
+                sw0 = *(const uint4_u*)ssrc;
+                sw1 = *(const uint4_u*)(ssrc + 16);
+            } else {
+                // the payload's last bytes: nothing past its end is read
+                uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                for (uint32_t j = 0; j < k; ++j) d[j >> 2] |= (uint32_t)ssrc[j] << (8 * (j & 3));
+                sw0 = make_uint4(d[0], d[1], d[2], d[3]);
+                sw1 = make_uint4(d[4], d[5], d[6], d[7]);
+            }
+            sp = true;
+            sp_dst = sdst;
+            ssrc += k;
+            sdst += k;
+            srem -= k;
+        }
+        if (cst) {
+            uint4 w = ref_fix(cw, csrc);
+            if (cst_pat) {
+                w = sym_pattern(w, cpd);
+                if (cpat_st == 1) {   // still the current match
+                    cpat = w;
+                    cpat_st = 2;
+                }
+            }
+            store_syms8(o, cdst, cap, w);
+            if (csz == 16) store_syms8(o, cdst + 8, cap, ref_fix(cw2, csrc + 8));
+            cst = false;
+            cst_pat = false;
+        }
+        if (bcnt) {
+            // the token's literal bytes as four symbols, one 8-byte store
+            const uint2 w = make_uint2((bval & 0xffu) | ((bval & 0xff00u) << 8),
+                                       ((bval >> 16) & 0xffu) | ((bval >> 8) & 0xff0000u));
+            if (bdst + 4 <= cap) {
+                *(uint2_s*)(o + bdst) = w;
+            } else {
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j)
+                    if (j < bcnt && bdst + j < cap) o[bdst + j] = (uint16_t)((bval >> (8 * j)) & 0xffu);
+            }
+            bcnt = 0;
+        }
+        if (crem) {
+            const uint32_t C = (cdist >= 16 && crem > 8) ? 16u : cdist >= 8 ? 8u : 0u;
+            bool ld = false;
+            int32_t src = 0;
+            if (C == 0) {
+                const uint32_t adv0 = 8 - 8 % cdist;
+                const uint32_t adv = adv0 < crem ? adv0 : crem;
+                if (cpat_st == 2) {
+                    store_syms8(o, cq, cap, cpat);
+                    cq += adv;
+                    crem -= adv;
+                } else if (cpat_st == 0) {
+                    ld = true;
+                    src = (int32_t)cq - 8;
+                    cst_pat = true;
+                    cpd = cdist;
+                    csz = 8;
+                    cpat_st = 1;
+                    cdst = cq;
+                    cq += adv;
+                    crem -= adv;
+                }
+            } else {
+                ld = true;
+                src = (int32_t)cq - (int32_t)cdist;
+                csz = C;
+                cdst = cq;
+                const uint32_t adv = C < crem ? C : crem;
+                cq += adv;
+                crem -= adv;
+            }
+            if (ld) {
+                cw = make_uint4(0, 0, 0, 0);
+                cw2 = cw;
+                if (src + 8 > 0) cw = *(const uint4_s*)(o + src);
+                if (csz == 16 && src + 16 > 0) cw2 = *(const uint4_s*)(o + src + 8);
+                csrc = src;
+                cst = true;
+            }
+        }
+        // ================================================ next token
+        if (!exited && crem == 0 && srem == 0) {
+            const uint32_t head = lds_load(T + O_HEAD);
+            compiler_fence();
+            uint2 e = make_uint2(0, 0);
+            if (tail != head) {
+                e = *(const uint2*)(T + ring_at(tail));
+                compiler_fence();
+            }
+            if (tail != head && !((e.y & TOK_NEW) && (cst || bcnt != 0 || sp))) {
+                ++tail;
+                lds_store(T + O_TAIL, tail);
+                worked = true;
+                if (e.y & TOK_END) {
+                    const uint32_t delta = (e.y >> 8) & 0x1fffffu;
+                    bp::SegRes r;
+                    r.nsym = e.x;
+                    r.status = (int32_t)(int8_t)(e.y & 0xffu);
+                    r.next = delta ? m + delta : 0xffffffffu;
+                    r.pad = 0;
+                    res[m] = r;
+                    done = true;
+                    exited = !queue;
+                } else if (e.y & TOK_NEW) {
+                    m = e.x;
+                    slot(m);
+                    pos = 0;
+                    done = false;
+                } else if (e.y & TOK_EXIT) {
+                    exited = true;
+                } else if (e.y & TOK_STORED) {
+                    srem = e.y & 0xffffu;
+                    ssrc = pl + e.x;
+                    sdst = pos;
+                    pos += srem;
+                } else {
+                    const uint32_t nl = e.y & 7u, ml = (e.y >> 3) & 511u;
+                    if (nl) {
+                        bcnt = nl;
+                        bdst = pos;
+                        bval = e.x;
+                        pos += nl;
+                    }
+                    if (ml) {
+                        crem = ml;
+                        cdist = (e.y >> 12) & 0xffffu;
+                        cq = pos;
+                        cpat_st = 0;
+                        pos += ml;
+                    }
+                }
+            }
+        }
+        if (!__ballot(worked)) __builtin_amdgcn_s_sleep(BPMD3_ESLEEP);
+    }
+    (void)done;
+}
+
 // ------------------------------------------------------------------- decoder
+// SEG: segment mode (block-parallel inflate, bp.h): the "messages" are
+// segment tasks; a lane starts at the task's bit, writes 16-bit symbols to
+// the task's slot (no window or capacity rule of the message: matches may
+// reach before the segment, the slot's end is SEG_FULL) and stops at the
+// block boundary that is the message's next candidate (SEG_HANDOFF).
+template <bool SEG>
 __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, const uint8_t* __restrict__ in,
                                         const uint64_t* __restrict__ in_off, const uint32_t* __restrict__ in_len,
                                         const uint32_t* __restrict__ out_cap, uint32_t raw,
                                         const uint32_t* __restrict__ mask_key, const uint32_t* __restrict__ hist_len,
                                         uint32_t hist_max, uint32_t n_msgs, const uint32_t* __restrict__ order,
-                                        uint32_t* __restrict__ qctr, uint32_t s0)
+                                        uint32_t* __restrict__ qctr, uint32_t s0,
+                                        const bp::SegTask* __restrict__ tasks)
 {
     uint32_t* H = (uint32_t*)(T + O_HIST);
     uint16_t* LE = (uint16_t*)(T + O_LE);
     const uint32_t tail = raw ? 0u : 4u;
-    const int32_t full_status = raw ? ST_OK : ST_NEED_BUFFERS;
+    const int32_t full_status = SEG ? bp::SEG_FULL : raw ? ST_OK : ST_NEED_BUFFERS;
+    // segment mode: payload bit of the view's first bit, the view's bits, and
+    // the next candidate of the message (task index, bit, slots after it)
+    uint32_t vbase = 0, vtot = 0, nk = 0, nk_bit = 0xffffffffu, nk_left = 0, nk_kind = 0;
+    const uint8_t* pl = in;   // the segment's payload
+    uint32_t pl_len = 0;
+    auto next_cand = [&](uint32_t from, uint32_t left) {
+        nk = 0;
+        nk_bit = 0xffffffffu;
+        nk_left = 0;
+        nk_kind = bp::KIND_NONE;
+        for (uint32_t j = 1; j <= left; ++j) {
+            const bp::SegTask& c = tasks[from + j];
+            if (c.kind != bp::KIND_NONE) {
+                nk = from + j;
+                nk_bit = c.bit;
+                nk_left = left - j;
+                nk_kind = c.kind;
+                break;
+            }
+        }
+    };
     // per-message state (set by begin())
     const uint8_t* A = in;
     uint32_t s = 0, n = 0, cap = 0, mk = 0, hist = 0;
@@ -559,20 +751,11 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
     uint32_t msg = m;
     bool send_new = false, send_exit = false, exhausted = qctr == nullptr;
     const uint32_t first_slots = s0 + gridDim.x * WG_MSGS;
-    auto begin = [&](uint32_t mm) {
-        msg = mm;
-        const uint8_t* p = in + in_off[mm];
-        n = in_len[mm];
-        cap = out_cap[mm];
+    // the bit reader over payload bytes [p, p + n) (+ the pmd tail)
+    auto open_view = [&](const uint8_t* p, uint32_t nn) {
+        n = nn;
         s = (uint32_t)((uintptr_t)p & 3);
         A = p - s;
-        // masked payloads (bpmd_read_batch): the dword at A + 4k holds payload
-        // bytes 4k - s .. 4k - s + 3, masked with key bytes (j - s) % 4
-        // (mask.ipp:38-59), so one rotation of the key unmasks every dword
-        mk = mask_key ? __builtin_amdgcn_alignbit(mask_key[mm], mask_key[mm], 8u * ((0u - s) & 3u)) : 0u;
-        // context takeover (bpmd_inflate_takeover_batch): the hist bytes before
-        // the slot are the window Beast's inflater keeps across messages
-        hist = hist_len ? (hist_len[mm] < hist_max ? hist_len[mm] : hist_max) : 0u;
         const uint4 b0w = issue_block(A, 0, s, n), b1w = issue_block(A, 1, s, n);
         q = finish_block(make_uint4(b0w.x ^ mk, b0w.y ^ mk, b0w.z ^ mk, b0w.w ^ mk), 0, s, n, tail);
         nx = finish_block(make_uint4(b1w.x ^ mk, b1w.y ^ mk, b1w.z ^ mk, b1w.w ^ mk), 1, s, n, tail);
@@ -588,9 +771,47 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
         tb = (int32_t)(8 * (s + n + tail));
         refill();
         refill();
-        drop(8 * s);
+    };
+    auto begin = [&](uint32_t mm) {
+        msg = mm;
+        uint32_t byte0 = 0, bit0 = 0, kind = 0;
+        bool skip = false;
+        if (SEG) {
+            // mm is a task: its message, first bit and slot
+            const bp::SegTask tk = tasks[mm];
+            skip = tk.kind == bp::KIND_NONE;
+            kind = tk.kind;
+            mm = skip ? 0u : tk.msg;
+            byte0 = skip ? 0u : tk.bit >> 3;
+            bit0 = skip ? 0u : tk.bit & 7u;
+            cap = tk.sym_cap;
+            next_cand(msg, skip ? 0u : tk.left);
+            pl = in + in_off[mm];
+            pl_len = in_len[mm];
+        }
+        if (!SEG) cap = out_cap[mm];
+        {
+            const uint8_t* p = in + in_off[mm] + byte0;
+            const uint32_t s_ = (uint32_t)((uintptr_t)p & 3);
+            // masked payloads (bpmd_read_batch): the dword at A + 4k holds payload
+            // bytes 4k - s .. 4k - s + 3, masked with key bytes (j - s) % 4
+            // (mask.ipp:38-59), so one rotation of the key unmasks every dword
+            mk = mask_key ? __builtin_amdgcn_alignbit(mask_key[mm], mask_key[mm], 8u * ((0u - s_) & 3u)) : 0u;
+            // context takeover (bpmd_inflate_takeover_batch): the hist bytes before
+            // the slot are the window Beast's inflater keeps across messages
+            hist = hist_len ? (hist_len[mm] < hist_max ? hist_len[mm] : hist_max) : 0u;
+            open_view(p, in_len[mm] - byte0);
+        }
+        drop(8 * s + bit0);
         st = raw && n == 0 ? S_DONE : S_TYPE;
         result = raw && n == 0 ? ST_NEED_BUFFERS : ST_OK;
+        if (SEG) {
+            vtot = 8 * (s + n + tail);
+            vbase = 8 * byte0 - 8 * s;
+            // a stored candidate starts at its LEN field (byte aligned)
+            st = skip ? S_DONE : kind == bp::KIND_STORED ? S_SHDR : st;
+            result = skip ? bp::SEG_SKIP : result;
+        }
         last = false;
         fin = false;
         pos = 0;
@@ -727,8 +948,8 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
         drop_x(mt && ev < 2 ? (is_match ? used + Ld + xd : used) : 0u);
         // output checks in the reference's order (inflate_stream.ipp:475-514)
         const bool tok = mt && ev == 0;
-        const bool c_raw = raw && pos >= cap;
-        const bool c_dist = is_match && dist > pos + hist;
+        const bool c_raw = !SEG && raw && pos >= cap;
+        const bool c_dist = !SEG && is_match && dist > pos + hist;
         const bool c_full = pos >= cap;
         uint32_t olen = is_match ? len : 1u;
         const bool c_trunc = pos + olen > cap;
@@ -797,7 +1018,7 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
         l3dyn_ += __builtin_popcountll(__ballot(st == S_DYN && !ring_empty));   // [7]
 #endif
         // this iteration's token
-        uint32_t enl = 0, elit = 0, emlen = 0, edist = 0;
+        uint32_t enl = 0, elit = 0, emlen = 0, edist = 0, estored = 0;
         const uint32_t st0 = st;
         const uint32_t head0 = head;
         L3_LAP(0);
@@ -810,6 +1031,16 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
         // is in a block's data or finished: a wave issues every instruction
         // of the section's per-state tests otherwise, exec-mask work included)
         if (__ballot(st0 != S_DATA && st0 != S_DONE)) {
+        if (SEG && st == S_TYPE && st0 == S_TYPE && !last) {
+            // a block boundary: the next candidate's header starts here, or
+            // candidates this segment has passed (not headers) are dropped
+            const uint32_t cur = vbase + (uint32_t)((int32_t)vtot - (tb + (int32_t)nb));
+            while (nk_bit < cur) next_cand(nk, nk_left);
+            if (nk_bit == cur && nk_kind == bp::KIND_DYN) {
+                result = bp::SEG_HANDOFF;
+                st = S_DONE;
+            }
+        }
         if (st == S_TYPE && st0 == S_TYPE) {
             if (last) {
                 result = ST_END_OF_STREAM;
@@ -877,7 +1108,17 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
             drop((uint32_t)avail & 7u);
             avail &= ~7;
             refill();
-            if (avail < 32) {
+            uint32_t cur = 0;
+            if (SEG) {
+                // the next candidate is this stored block (its LEN field)
+                cur = vbase + (uint32_t)((int32_t)vtot - avail);
+                if (nk_bit == cur && nk_kind == bp::KIND_STORED) {
+                    result = bp::SEG_HANDOFF;
+                    st = S_DONE;
+                }
+            }
+            if (st != S_SHDR) {
+            } else if (avail < 32) {
                 st = S_DONE;
             } else {
                 const uint32_t v = (uint32_t)bb & 0xffffu, nv = (uint32_t)(bb >> 16) & 0xffffu;
@@ -897,6 +1138,29 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
                     sstarve = nc < v;
                     srem = nc;
                     st = S_SCOPY;
+                    if (SEG && room && (cur >> 3) + 4 + nc <= pl_len) {
+                        // segment mode: the expander copies the block's bytes
+                        // from the input (one token); the reader moves past
+                        // them.  (Data reaching into the pmd tail goes the
+                        // byte way: the tail is not in memory.)
+                        const uint32_t from = (cur >> 3) + 4;   // payload byte of the data
+                        estored = nc;
+                        elit = from;
+                        pos += nc;
+                        srem = 0;
+                        if (sfull) {
+                            result = full_status;
+                            st = S_DONE;
+                        } else if (sstarve) {
+                            st = S_DONE;
+                        } else {
+                            open_view(pl + from + nc, pl_len - from - nc);
+                            drop(8 * s);
+                            vtot = 8 * (s + n + tail);
+                            vbase = 8 * (from + nc) - 8 * s;
+                            st = S_TYPE;
+                        }
+                    }
                 }
             }
         }
@@ -1157,12 +1421,14 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
         // (selects rather than an if-chain: one predicated store, one head store)
         {
             const bool ctl = send_new || send_exit;       // NEW / EXIT (work queue)
-            const bool data = !ctl && (enl || emlen);     // produced only with room
+            const bool data = !ctl && (enl || emlen || estored);   // produced only with room
             const bool endt = !ctl && !data && st == S_DONE && !fin;
             const bool adv = room && (ctl || data || endt);
+            const uint32_t hand = SEG && result == bp::SEG_HANDOFF ? (nk - msg) << 8 : 0u;
             const uint2 ent = ctl    ? make_uint2(msg, send_new ? TOK_NEW : TOK_EXIT)
-                              : data ? make_uint2(elit, enl | (emlen << 3) | (edist << 12))
-                                     : make_uint2(pos, TOK_END | ((uint32_t)result & 0xffu));
+                              : data ? make_uint2(elit, estored ? (TOK_STORED | estored)
+                                                                : (enl | (emlen << 3) | (edist << 12)))
+                                     : make_uint2(pos, TOK_END | hand | ((uint32_t)result & 0xffu));
             if (adv) *(uint2*)(T + ring_at(head)) = ent;
             compiler_fence();
             head += adv ? 1u : 0u;
@@ -1239,14 +1505,53 @@ inflate_lane3_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict_
     __syncthreads();
     if (is_decoder) {
         if (BPMD3_DPRIO) __builtin_amdgcn_s_setprio(BPMD3_DPRIO);   // the decoder sets the pace
-        decoder(T, valid, m, in, in_off, in_len, out_cap, raw, mask_key, hist_len, hist_max, n_msgs, order, qctr, s0);
+        decoder<false>(T, valid, m, in, in_off, in_len, out_cap, raw, mask_key, hist_len, hist_max, n_msgs, order, qctr,
+                       s0, nullptr);
     } else {
         expander(T, valid, m, out, out_off, out_cap, out_len, status, hist_len, hist_max, qctr != nullptr);
     }
 }
 
+// Segment mode (block-parallel inflate, pmd_inflate_bp.hip): the same
+// decoder / expander pair over segment tasks.
+__global__ void __launch_bounds__(128, 2)
+inflate_lane3_seg_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                         const uint32_t* __restrict__ in_len, uint32_t n_tasks, const bp::SegTask* __restrict__ tasks,
+                         uint16_t* __restrict__ sym, bp::SegRes* __restrict__ res, uint32_t raw,
+                         uint32_t* __restrict__ qctr)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const unsigned lane = threadIdx.x & 63u;
+    const bool is_decoder = threadIdx.x < 64;
+    uint8_t* T = smem + lane * STRIDE;
+    const uint32_t j = blockIdx.x * WG_MSGS + lane;
+    const bool valid = j < n_tasks;
+    if (is_decoder) *(uint2*)(T + O_HEAD) = make_uint2(0, 0);
+    __syncthreads();
+    if (is_decoder) {
+        if (BPMD3_DPRIO) __builtin_amdgcn_s_setprio(BPMD3_DPRIO);
+        decoder<true>(T, valid, valid ? j : 0u, in, in_off, in_len, nullptr, raw, nullptr, nullptr, 0u, n_tasks, nullptr,
+                      qctr, 0u, tasks);
+    } else {
+        expander_seg(T, valid, valid ? j : 0u, sym, tasks, res, qctr != nullptr, in, in_off, in_len);
+    }
+}
+
 }  // namespace lp3
 }  // namespace bpmd
+
+extern "C" int bpmd_internal_inflate_lane3_seg(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                               uint32_t n_tasks, const void* tasks, uint16_t* sym, void* res,
+                                               uint32_t raw, uint32_t* qctr, uint32_t grid_wgs, hipStream_t stream)
+{
+    using namespace bpmd::lp3;
+    if (n_tasks == 0) return 0;
+    unsigned grid = (n_tasks + WG_MSGS - 1) / WG_MSGS;
+    if (qctr && grid_wgs && grid > grid_wgs) grid = grid_wgs;
+    hipLaunchKernelGGL(inflate_lane3_seg_kernel, dim3(grid), dim3(128), WG_MSGS * STRIDE, stream, in, in_off, in_len,
+                       n_tasks, (const bpmd::bp::SegTask*)tasks, sym, (bpmd::bp::SegRes*)res, raw, qctr);
+    return (int)hipGetLastError();
+}
 
 // order: NULL or the order messages are taken in (e.g. longest first);
 // qctr: NULL (one message per lane) or a zeroed device counter: then the grid
@@ -1338,13 +1643,17 @@ __global__ void __launch_bounds__(256) sum_in_kernel(const uint32_t* __restrict_
     for (int d = 32; d >= 1; d >>= 1) acc += __shfl_down(acc, d);
     if ((threadIdx.x & 63) == 0 && acc) atomicAdd(total, acc);
 }
-__global__ void long_count_kernel(const uint32_t* __restrict__ keys, uint32_t n, uint32_t lanes,
+__global__ void long_count_kernel(const uint32_t* __restrict__ keys, uint32_t n, uint32_t lanes, uint32_t min_thr,
                                   unsigned long long* __restrict__ split)
 {
     if (threadIdx.x != 0) return;
+    if (min_thr == 0 && lanes == 0) {   // every payload
+        ((uint32_t*)split)[2] = n;
+        return;
+    }
     const unsigned long long total = split[0];
-    unsigned long long thr = 2ull * total / (lanes ? lanes : 1u);
-    if (thr < 4096) thr = 4096;
+    unsigned long long thr = lanes ? 2ull * total / lanes : 0ull;
+    if (thr < min_thr) thr = min_thr;
     const uint32_t tk = (uint32_t)((thr + 63) >> 6);   // long: key > tk (keys descending)
     uint32_t lo = 0, hi = n;
     while (lo < hi) {
@@ -1358,15 +1667,16 @@ __global__ void long_count_kernel(const uint32_t* __restrict__ keys, uint32_t n,
 }  // namespace bpmd
 
 // returns a device pointer to the number of long payloads (a prefix of the
-// order bpmd_internal_lane_order returned with `keys`), or null on error
+// order bpmd_internal_lane_order returned with `keys`), or null on error.
+// lanes == 0: a fixed threshold of min_thr compressed bytes (0: every payload).
 extern "C" const uint32_t* bpmd_internal_lane_long_split(const uint32_t* in_len, const uint32_t* keys, uint32_t n,
-                                                         uint32_t lanes, hipStream_t stream)
+                                                         uint32_t lanes, uint32_t min_thr, hipStream_t stream)
 {
     unsigned long long* split = (unsigned long long*)bpmd_internal_scratch(stream, 256, 9);
     if (!split || hipMemsetAsync(split, 0, 16, stream) != hipSuccess) return nullptr;
     const uint32_t blocks = n / 256 + 1 < 1024 ? n / 256 + 1 : 1024;
     hipLaunchKernelGGL(bpmd::lp3::sum_in_kernel, dim3(blocks), dim3(256), 0, stream, in_len, n, split);
-    hipLaunchKernelGGL(bpmd::lp3::long_count_kernel, dim3(1), dim3(64), 0, stream, keys, n, lanes, split);
+    hipLaunchKernelGGL(bpmd::lp3::long_count_kernel, dim3(1), dim3(64), 0, stream, keys, n, lanes, min_thr, split);
     if (hipGetLastError() != hipSuccess) return nullptr;
     return (const uint32_t*)split + 2;
 }

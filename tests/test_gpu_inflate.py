@@ -14,14 +14,15 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 
-@pytest.fixture(autouse=True, params=["lane", "wave", "wave_walk", "wave_spec"])
+@pytest.fixture(autouse=True, params=["lane", "wave", "wave_walk", "wave_spec", "bp"])
 def inflate_kernel(request):
     """Every inflate test runs on both kernels (pmd_inflate_lane3.hip and
     pmd_inflate.hip), forced through bpmd_set_inflate_kernel; the wave kernel
     also with every round a walk round and with speculative rounds only
-    (bpmd_diag_set_wave_walk)."""
+    (bpmd_diag_set_wave_walk); and block-parallel (pmd_inflate_bp.hip: every
+    payload of 64 bytes or more cut at its dynamic-block headers)."""
     pmd = _pmd()
-    mode = {"lane": 1, "wave": 2, "wave_walk": 2, "wave_spec": 2}[request.param]
+    mode = {"lane": 1, "wave": 2, "wave_walk": 2, "wave_spec": 2, "bp": 3}[request.param]
     walk = {"wave_walk": 1, "wave_spec": 2}.get(request.param, 0)
     assert pmd.lib().bpmd_set_inflate_kernel(mode) == 0
     assert pmd.lib().bpmd_diag_set_wave_walk(walk) == 0

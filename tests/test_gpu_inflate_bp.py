@@ -1,0 +1,169 @@
+"""Block-parallel inflate of long payloads (pmd_inflate_bp.hip): payloads cut
+at their dynamic-block headers, segments decoded one per lane as symbols,
+resolved in stream order.  Bytes, lengths and statuses must equal the
+oracle's serial inflate (oracle/bzo_inflate.c, inflate_stream.ipp) exactly,
+including the first invalid distance, the output capacity and decode errors
+wherever they fall relative to the segment boundaries."""
+import random
+import zlib
+
+import numpy as np
+import pytest
+
+from beast_amd import synth
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _pmd():
+    import torch  # noqa: F401
+    from beast_amd import pmd
+    return pmd
+
+
+@pytest.fixture(params=["bp", "auto"])
+def mode(request):
+    pmd = _pmd()
+    assert pmd.lib().bpmd_set_inflate_kernel({"bp": 3, "auto": 0}[request.param]) == 0
+    yield request.param
+    pmd.lib().bpmd_set_inflate_kernel(0)
+
+
+def _run(payloads, caps, raw=False):
+    import torch
+    pmd = _pmd()
+    src = pmd.Batch.from_host(payloads)
+    c = caps if isinstance(caps, int) else torch.tensor(caps, dtype=torch.int32)
+    res = pmd.inflate_batch(src, c, raw=raw)
+    torch.cuda.synchronize()
+    return res.status.cpu().numpy(), res.out.to_host()
+
+
+def _check(payloads, caps, raw=False):
+    st, outs = _run(payloads, caps, raw=raw)
+    for i, p in enumerate(payloads):
+        cap = caps if isinstance(caps, int) else caps[i]
+        est, eout = O.pmd_inflate(p, cap=cap, raw=raw)
+        assert int(st[i]) == est, (i, O.ERRORS[int(st[i])], O.ERRORS[est], len(p), cap)
+        assert outs[i] == eout, (i, len(outs[i]), len(eout), cap)
+
+
+def _data(kind, size, seed):
+    d, _, _ = synth.make_batch(kind, [size], seed=seed)
+    return bytes(d[:size])
+
+
+@pytest.mark.parametrize("level", [1, 6, 9])
+@pytest.mark.parametrize("mem", [1, 4, 9])
+def test_long_payloads_beast_blocks(mode, level, mem):
+    """Beast's own payloads (the oracle's deflate_stream): blocks every
+    lit_bufsize - 1 symbols, stored / fixed / dynamic mixed."""
+    payloads, caps = [], []
+    for kind in ("json", "binary", "corpus1", "random"):
+        for size in (9000, 40000, 65536, 150000):
+            data = _data(kind, size, level * 1000 + mem * 10 + size)
+            payloads.append(O.pmd_deflate(data, level, 15, mem))
+            caps.append(size)
+    _check(payloads, caps)
+    _check(payloads, caps, raw=True)
+
+
+def test_long_payloads_gpu_deflater(mode):
+    """This library's chunk-parallel deflater (one block per 4 KiB chunk)."""
+    import torch
+    pmd = _pmd()
+    sizes = [65536] * 24 + [30000] * 8 + [200000] * 2
+    kinds = ["binary", "json", "corpus1"]
+    payloads = []
+    for i, size in enumerate(sizes):
+        data = _data(kinds[i % 3], size, 77 + i)
+        src = pmd.Batch.from_host([data])
+        res = pmd.deflate_batch(src, level=1 + (i % 2) * 5)
+        torch.cuda.synchronize()
+        assert int(res.status[0]) == 0
+        payloads.append(res.out.to_host()[0])
+    _check(payloads, sizes)
+
+
+def test_capacity_cuts_across_segments(mode):
+    """The capacity rule at every kind of position: inside segments, at their
+    boundaries, at the exact size and past it."""
+    data = _data("json", 120000, 11)
+    p = O.pmd_deflate(data, 6, 15, 1)   # 64-symbol blocks: many candidates
+    rng = random.Random(3)
+    caps = sorted({1, 4095, 4096, 4097, 65535, 65536, 119999, 120000, 120001} |
+                  {rng.randrange(1, 120000) for _ in range(40)})
+    _check([p] * len(caps), caps)
+    _check([p] * len(caps), caps, raw=True)
+
+
+def test_preset_dictionary_distances(mode):
+    """Distances past the start of the message (a peer that used a preset
+    dictionary): invalid_distance at the first such token, whichever segment
+    holds it, and the capacity rule when the output is full first."""
+    rng = random.Random(5)
+    zd = rng.randbytes(32768)
+    payloads, caps = [], []
+    for lead in (0, 3000, 9000, 20000, 28000):
+        data = bytearray(rng.randbytes(lead))
+        while len(data) < 40000:
+            k = rng.randrange(0, 32768 - 64)
+            data += zd[k:k + rng.randrange(16, 64)] + rng.randbytes(rng.randrange(200, 2000))
+        for level, mem in ((6, 4), (1, 1), (9, 8)):
+            c = zlib.compressobj(level, zlib.DEFLATED, -15, mem, zdict=zd)
+            comp = c.compress(bytes(data)) + c.flush(zlib.Z_SYNC_FLUSH)
+            assert comp.endswith(b"\x00\x00\xff\xff")
+            payloads.append(comp[:-4])
+            caps.append(len(data))
+            payloads.append(comp[:-4])
+            caps.append(max(1, lead - 7))
+    _check(payloads, caps)
+
+
+def test_corrupted_long_payloads(mode):
+    rng = random.Random(9)
+    base = [O.pmd_deflate(_data(k, 50000, i), rng.choice([1, 6]), 15, 4)
+            for i, k in enumerate(("json", "binary", "corpus1"))]
+    payloads = []
+    for _ in range(150):
+        q = bytearray(rng.choice(base))
+        if rng.randrange(2):
+            for _ in range(rng.randrange(1, 4)):
+                q[rng.randrange(len(q))] ^= 1 << rng.randrange(8)
+        else:
+            q = q[:rng.randrange(64, len(q))]
+        payloads.append(bytes(q))
+    _check(payloads, 60000)
+    _check(payloads, 60000, raw=True)
+
+
+def test_highly_compressible_falls_back(mode):
+    """Output far above the per-segment estimate (zeros, runs): the segment
+    slot fills and the payload is decoded again by the wave kernel."""
+    payloads, caps = [], []
+    for kind, size in (("zeros", 500000), ("corpus1", 300000), ("zeros", 70000)):
+        data = _data(kind, size, size)
+        payloads.append(O.pmd_deflate(data, 6, 15, 8))
+        caps.append(size)
+    _check(payloads, caps)
+
+
+def test_auto_mixed_batch_takes_bp():
+    """Automatic mode, 2 100 messages: the long ones go block-parallel, the
+    rest to the lane kernel, all in one call."""
+    pmd = _pmd()
+    assert pmd.lib().bpmd_set_inflate_kernel(0) == 0
+    rng = random.Random(13)
+    payloads, caps = [], []
+    for i in range(2100):
+        if i % 7 == 0:
+            size = rng.choice([20000, 65536])
+            kind = rng.choice(["binary", "json"])
+        else:
+            size = rng.randrange(100, 4000)
+            kind = "json"
+        data = _data(kind, size, 1000 + i)
+        payloads.append(O.pmd_deflate(data, rng.choice([1, 6]), 15, 4))
+        caps.append(size)
+    _check(payloads, caps)
