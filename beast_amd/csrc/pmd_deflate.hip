@@ -1335,6 +1335,23 @@ stitch_kernel(const uint32_t* __restrict__ in_len, uint32_t n, uint32_t all, con
                 bit = (P + nbytes) * 8;
                 cv = 0;
             } else {
+                if (c) {
+                    // a marker before every Huffman-coded chunk but the first:
+                    // an empty stored block (000, pad, 00 00 FF FF), so the
+                    // block starts on a byte that a block-parallel inflater
+                    // finds by a byte search (pmd_inflate_bp.hip); ~5 bytes
+                    // per 4 KiB chunk
+                    const uint32_t P = (bit + 3 + 7) >> 3;
+                    if (P + 4 + 1 > cap) { overflow = true; break; }
+                    if (lane == 0) {
+                        o[B] = (uint8_t)cv ^ km(B);
+                        if (P - B == 2) o[B + 1] = km(B + 1);
+                    }
+                    if (lane < 4) o[P + lane] = (uint8_t)(lane < 2 ? 0x00 : 0xff) ^ km(P + lane);
+                    bit = (P + 4) * 8;
+                    cv = 0;
+                }
+                const uint32_t B = bit >> 3, s = bit & 7;
                 const uint32_t end = bit + L;
                 if (((end + 7) >> 3) + 1 > cap) { overflow = true; break; }
                 const uint32_t nb = (L + 7) >> 3;             // slot bytes

@@ -74,8 +74,23 @@ struct Stat {
 };
 
 __global__ void __launch_bounds__(256)
+bp_sum_kernel(const uint32_t* __restrict__ in_len, const uint32_t* __restrict__ order,
+              const uint32_t* __restrict__ nlong, uint32_t n, unsigned long long* __restrict__ total)
+{
+    unsigned long long acc = 0;
+    const uint32_t nl = *nlong;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nl && i < n; i += gridDim.x * 256u) acc += in_len[order[i]];
+    for (int d = 32; d >= 1; d >>= 1) acc += __shfl_down(acc, d);
+    if ((threadIdx.x & 63) == 0 && acc) atomicAdd(total, acc);
+}
+
+// Region size: about SEG_OUT of output at the payload's provisioned ratio,
+// but no smaller than the batch's long bytes over 2 segments per lane of
+// the chip (more segments only cost scanning once every lane has two).
+__global__ void __launch_bounds__(256)
 bp_stats_kernel(const uint32_t* __restrict__ in_len, const uint32_t* __restrict__ out_cap,
                 const uint32_t* __restrict__ order, const uint32_t* __restrict__ nlong, uint32_t n,
+                const unsigned long long* __restrict__ total, uint32_t lanes,
                 Stat* __restrict__ st, uint32_t* __restrict__ regions, unsigned long long* __restrict__ words)
 {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
@@ -89,6 +104,8 @@ bp_stats_kernel(const uint32_t* __restrict__ in_len, const uint32_t* __restrict_
         // output per compressed byte the caller provisioned, capped at 4
         const uint64_t e16 = cap >= 4ull * len ? (4ull << 16) : (((uint64_t)cap << 16) / (len ? len : 1u));
         uint64_t R = cap ? ((uint64_t)SEG_OUT * len) / cap : R_MAX;
+        const uint64_t share = *total / (2ull * (lanes ? lanes : 1u));
+        R = R < share ? share : R;
         R = R < R_MIN ? R_MIN : R > R_MAX ? R_MAX : R;
         R &= ~255ull;
         na = (uint32_t)((len + R - 1) / R);
@@ -262,14 +279,22 @@ __device__ bool dyn_header_ok(const Bits& B, uint32_t b, uint32_t lim)
 // and what follows must check out: the payload's end, another stored block,
 // or a dynamic header passing dyn_header_ok.  (A stored block followed by a
 // fixed-Huffman block is not a segment start: nothing validates the latter.)
-__device__ bool stored_ok(const GlobalBits& G, uint32_t s, uint32_t len, uint32_t pb, uint32_t L)
+// (The staged region holds the next header when it starts inside the
+// region's stage -- always for this library's markers -- else it is read
+// from global memory.)
+__device__ bool stored_ok(const GlobalBits& G, const LdsBits& Lb, uint32_t bias, uint32_t lim, uint32_t s,
+                          uint32_t len, uint32_t pb, uint32_t L)
 {
     const uint32_t q = pb + 4 + L;   // the next block's first byte
     if (q > len) return false;
     if (q == len) return true;
     const uint32_t h = G.peek(8 * (s + q));
     const uint32_t type = (h >> 1) & 3u;
-    if (type == 2) return dyn_header_ok(G, 8 * (s + q), 8 * (s + len));
+    if (type == 2) {
+        const uint32_t lq = 8 * q + bias;   // the header's LDS bit
+        if (lq + 2400 <= lim || lim - (8 * len + bias) == 0) return dyn_header_ok(Lb, lq, lim);
+        return dyn_header_ok(G, 8 * (s + q), 8 * (s + len));
+    }
     if (type == 0) {
         if (q + 5 > len) return false;
         const uint32_t w = G.peek(8 * (s + q + 1));
@@ -369,7 +394,8 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
                         const uint32_t pb = (first >> 3) + j;
                         const bool c = first + 8 * j < b1 && ((x & 0xffffu) ^ (x >> 16)) == 0xffffu &&
                                        (prevb & 0xc0u) == 0 && pb + 4 + (x & 0xffffu) <= len;
-                        if (c && found == 0xffffffffu && stored_ok(G, s, len, pb, x & 0xffffu)) found = 8 * pb;
+                        if (c && found == 0xffffffffu && stored_ok(G, Lb, bias, lim, s, len, pb, x & 0xffffu))
+                            found = 8 * pb;
                     }
                     const uint64_t fm = __ballot(found != 0xffffffffu);
                     if (fm) {
@@ -689,6 +715,7 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
     const size_t o_st = 0, o_reg = al256(o_st + sizeof(Stat) * (size_t)n), o_tb = al256(o_reg + 4ull * n),
                  o_w = al256(o_tb + 4ull * n), o_wb = al256(o_w + 8ull * n), o_tot = al256(o_wb + 8ull * n),
                  o_q = al256(o_tot + sizeof(Totals)), o_tmp = al256(o_q + 64), sz = al256(o_tmp + (tmp1 > tmp2 ? tmp1 : tmp2));
+    // q: [0] scan queue, [1] resolve queue, [2] fallback count, [3] seg queue, [4-5] long bytes
     uint8_t* ws = (uint8_t*)bpmd_internal_scratch(s, sz, 10);
     if (!ws) return (int)hipErrorOutOfMemory;
     Stat* st = (Stat*)(ws + o_st);
@@ -699,15 +726,21 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
     Totals* dtot = (Totals*)(ws + o_tot);
     uint32_t* q = (uint32_t*)(ws + o_q);   // [0] scan queue, [1] resolve queue, [2] fallback count, [3] seg queue
     void* tmp = ws + o_tmp;
-    hipLaunchKernelGGL(bp_stats_kernel, dim3((n + 255) / 256), dim3(256), 0, s, in_len, out_cap, order, nlong, n, st,
-                       reg, words);
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    unsigned long long* total = (unsigned long long*)(q + 4);
+    if (hipMemsetAsync(q, 0, 64, s) != hipSuccess) return (int)hipErrorUnknown;
+    hipLaunchKernelGGL(bp_sum_kernel, dim3(n / 256 + 1 < 1024 ? n / 256 + 1 : 1024), dim3(256), 0, s, in_len, order,
+                       nlong, n, total);
+    hipLaunchKernelGGL(bp_stats_kernel, dim3((n + 255) / 256), dim3(256), 0, s, in_len, out_cap, order, nlong, n, total,
+                       256u * (uint32_t)cus, st, reg, words);
     if (hipGetLastError() != hipSuccess) return (int)hipErrorUnknown;
     size_t t1 = tmp1, t2 = tmp2;
     if (hipcub::DeviceScan::ExclusiveSum(tmp, t1, reg, tbase, (int)n, s) != hipSuccess ||
         hipcub::DeviceScan::ExclusiveSum(tmp, t2, words, wbase, (int)n, s) != hipSuccess)
         return (int)hipErrorUnknown;
     hipLaunchKernelGGL(bp_totals_kernel, dim3(1), dim3(64), 0, s, reg, tbase, words, wbase, n, dtot);
-    if (hipGetLastError() != hipSuccess || hipMemsetAsync(q, 0, 64, s) != hipSuccess ||
+    if (hipGetLastError() != hipSuccess ||
         hipMemcpyAsync(H.tot, dtot, sizeof(Totals), hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipEventRecord(H.ev, s) != hipSuccess || hipEventSynchronize(H.ev) != hipSuccess)
         return (int)hipErrorUnknown;
@@ -723,8 +756,6 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
     SegRes* res = (SegRes*)(dw + d_res);
     uint32_t* fb = (uint32_t*)(dw + d_fb);
     uint16_t* sym = (uint16_t*)(dw + d_sym);
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     // scan: SCAN_WAVES waves per workgroup, ~3 workgroups per CU by LDS
     const uint32_t scan_wgs = 3u * (uint32_t)cus;
     hipLaunchKernelGGL(bp_scan_kernel, dim3(scan_wgs), dim3(64 * SCAN_WAVES), 0, s, in, in_off, in_len, order, nlong,

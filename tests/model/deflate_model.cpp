@@ -146,6 +146,15 @@ static std::vector<uint8_t> encode(const uint8_t* msg, unsigned n, const Params&
     unsigned max_dist = wsize - LOOKAHEAD_MIN;
     std::vector<int32_t> prev;
     std::vector<int32_t> head(1u << P.hbits);
+    // the stitch's marker before every Huffman-coded chunk but the first: an
+    // empty stored block, so the block starts on a byte
+    auto marker = [&](unsigned base) {
+        if (!base) return;
+        bw.put(0, 3);
+        bw.align();
+        bw.put(0, 16);
+        bw.put(0xFFFF, 16);
+    };
     for (unsigned base = 0; base < n; base += P.chunk) {
         unsigned cend = base + P.chunk < n ? base + P.chunk : n;
         unsigned wb = base > (unsigned)P.hist ? base - P.hist : 0;
@@ -238,6 +247,7 @@ static std::vector<uint8_t> encode(const uint8_t* msg, unsigned n, const Params&
             bw.put(~clen & 0xFFFF, 16);
             for (unsigned q = 0; q < clen; ++q) bw.put(msg[base + q], 8);
         } else if (fix_b <= opt_b) {
+            marker(base);
             for (int s = 0; s < N_LCODES + 2; ++s) fix.llen[s] = (uint8_t)fixed_lit_len(s);
             for (int s = 0; s < N_DCODES; ++s) fix.dlen[s] = 5;
             canonical_codes_host(fix.llen, N_LCODES + 2, fix.lcode);
@@ -247,6 +257,7 @@ static std::vector<uint8_t> encode(const uint8_t* msg, unsigned n, const Params&
         } else {
             canonical_codes_host(dyn.llen, N_LCODES, dyn.lcode);
             canonical_codes_host(dyn.dlen, N_DCODES, dyn.dcode);
+            marker(base);
             bw.put(2 << 1, 3);
             bw.put(lcodes - 257, 5);
             bw.put(dcodes - 1, 5);
