@@ -108,7 +108,8 @@ bp_stats_kernel(const uint32_t* __restrict__ in_len, const uint32_t* __restrict_
         R = R < share ? share : R;
         R = R < R_MIN ? R_MIN : R > R_MAX ? R_MAX : R;
         R &= ~255ull;
-        na = (uint32_t)((len + R - 1) / R);
+        na = (uint32_t)((len + R / 2) / R);   // a last region shorter than R / 2 joins the one before
+        na = na ? na : 1u;
         s.regions = na;
         s.R = (uint32_t)R;
         s.F16 = (uint32_t)((e16 * 5) >> 2);
@@ -136,6 +137,18 @@ __global__ void bp_totals_kernel(const uint32_t* __restrict__ regions, const uin
         tot->words = word_base[n - 1] + words[n - 1];
     }
 }
+
+// diagnostics (bpmd_diag_bp_counters): [0] payloads resolved, [1] segments
+// on their chains, [2] payloads sent to the wave kernel; with -DBPMD_BP_DIAG
+// (contended atomics: timing changes) also [4] regions scanned, [5] found a
+// stored block, [6] searched for dynamic headers, [7] full dynamic-header
+// checks, [8-10] scan cycles staging / stored search / dynamic search
+#ifdef BPMD_BP_DIAG
+#define BP_DIAG(x) x
+#else
+#define BP_DIAG(x)
+#endif
+__device__ unsigned long long g_bp_diag[12];
 
 // ------------------------------------------------------------------ scan
 __device__ __forceinline__ uint32_t wave_lane() { return threadIdx.x & 63u; }
@@ -273,36 +286,6 @@ __device__ bool dyn_header_ok(const Bits& B, uint32_t b, uint32_t lim)
     return true;
 }
 
-// Is there a stored block whose LEN field is payload byte pb (LEN == ~NLEN,
-// checked by the caller)?  The bits before it must be the zero padding and
-// block type every encoder writes, the block must end inside the payload,
-// and what follows must check out: the payload's end, another stored block,
-// or a dynamic header passing dyn_header_ok.  (A stored block followed by a
-// fixed-Huffman block is not a segment start: nothing validates the latter.)
-// (The staged region holds the next header when it starts inside the
-// region's stage -- always for this library's markers -- else it is read
-// from global memory.)
-__device__ bool stored_ok(const GlobalBits& G, const LdsBits& Lb, uint32_t bias, uint32_t lim, uint32_t s,
-                          uint32_t len, uint32_t pb, uint32_t L)
-{
-    const uint32_t q = pb + 4 + L;   // the next block's first byte
-    if (q > len) return false;
-    if (q == len) return true;
-    const uint32_t h = G.peek(8 * (s + q));
-    const uint32_t type = (h >> 1) & 3u;
-    if (type == 2) {
-        const uint32_t lq = 8 * q + bias;   // the header's LDS bit
-        if (lq + 2400 <= lim || lim - (8 * len + bias) == 0) return dyn_header_ok(Lb, lq, lim);
-        return dyn_header_ok(G, 8 * (s + q), 8 * (s + len));
-    }
-    if (type == 0) {
-        if (q + 5 > len) return false;
-        const uint32_t w = G.peek(8 * (s + q + 1));
-        return ((w & 0xffffu) ^ (w >> 16)) == 0xffffu;
-    }
-    return false;
-}
-
 // Kraft sum x 128 of four 3-bit code-length-code lengths (0 = unused)
 __device__ __forceinline__ uint32_t kraft4(uint32_t f)
 {
@@ -313,6 +296,54 @@ __device__ __forceinline__ uint32_t kraft4(uint32_t f)
         k += l ? 128u >> l : 0u;
     }
     return k;
+}
+
+// Could a dynamic-block header start at bit b?  Block type 2, HLIT <= 29,
+// HDIST <= 29 and a complete code-length code (about 1 in 1 000 random
+// offsets pass).
+template <class Bits>
+__device__ __forceinline__ bool dyn_header_quick(const Bits& B, uint32_t b, uint32_t lim)
+{
+    if (b + 17 + 57 > lim) return false;
+    const uint32_t h = B.peek(b);
+    if (((h >> 1) & 3u) != 2u || ((h >> 3) & 31u) > 29u || ((h >> 8) & 31u) > 29u) return false;
+    const uint32_t ncode = ((h >> 13) & 15u) + 4;
+    const uint32_t a = B.peek(b + 17), c = B.peek(b + 47);
+    const uint64_t x = (uint64_t)(a & 0x3fffffffu) | ((uint64_t)c << 30);
+    uint32_t kr = 0;
+    for (uint32_t i = 0; i < ncode; ++i) {
+        const uint32_t l = (uint32_t)(x >> (3 * i)) & 7u;
+        kr += l ? 128u >> l : 0u;
+    }
+    return kr == 128u;
+}
+
+// Is there a stored block whose LEN field is payload byte pb (LEN == ~NLEN,
+// checked by the caller)?  The bits before it must be the zero padding and
+// block type every encoder writes (checked by the caller), the block must end
+// inside the payload, and what follows must look like a block: the payload's
+// end, another stored block, a plausible dynamic header, or -- after an
+// empty block (a sync-flush marker, 2^-34 per random byte) -- a fixed one.
+// A false start would only cost a wasted lane (its slot is its own) ... and
+// its rate here is below 1 in 10^12 per byte.
+__device__ bool stored_ok(const GlobalBits& G, const LdsBits& Lb, uint32_t bias, uint32_t lim, uint32_t s,
+                          uint32_t len, uint32_t pb, uint32_t L)
+{
+    const uint32_t q = pb + 4 + L;   // the next block's first byte
+    if (q > len) return false;
+    if (q == len) return true;
+    const uint32_t lq = 8 * q + bias;   // the next header's LDS bit, when staged
+    const bool staged = lq + 96 <= lim;
+    const uint32_t h = staged ? Lb.peek(lq) : G.peek(8 * (s + q));
+    const uint32_t type = (h >> 1) & 3u;
+    if (type == 2)
+        return staged ? dyn_header_quick(Lb, lq, lim) : dyn_header_quick(G, 8 * (s + q), 8 * (s + len));
+    if (type == 0) {
+        if (q + 5 > len) return false;
+        const uint32_t w = staged && lq + 8 + 32 <= lim ? Lb.peek(lq + 8) : G.peek(8 * (s + q + 1));
+        return ((w & 0xffffu) ^ (w >> 16)) == 0xffffu;
+    }
+    return type == 1 && L == 0;
 }
 
 constexpr uint32_t LIST = 128;         // candidate offsets per wave and chunk
@@ -359,23 +390,41 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
             uint32_t bit = 0, kind = KIND_START;
             if (k) {
                 kind = KIND_NONE;
+                BP_DIAG(const uint64_t t0 = __builtin_amdgcn_s_memtime());
                 // stage payload bytes from the dword before the region's first
                 // byte (so every offset has its previous byte) to STAGE_EXTRA
                 // past its end, as dwords; bytes past the payload read as zeros
                 const uint32_t q0 = ((s + k * st.R) >> 2) - 1;
                 const uint32_t nwords = STAGE_BYTES / 4 + 8;
                 const uint32_t tailm = ((s + len) & 3u) ? (1u << (8 * ((s + len) & 3u))) - 1u : ~0u;
-                for (uint32_t j = lane; j < nwords; j += 64)
-                    S[j] = q0 + j < E ? (q0 + j == E - 1 ? A[q0 + j] & tailm : A[q0 + j]) : 0u;
+                // only the words this region's size needs are loaded
+                const uint32_t nw = (st.R + STAGE_EXTRA + 64) / 4 < nwords ? (st.R + STAGE_EXTRA + 64) / 4 : nwords;
+                {
+                    // all loads in flight together (a load-store loop would
+                    // wait out one memory latency per dword)
+                    constexpr uint32_t U = (STAGE_BYTES / 4 + 8 + 63) / 64;
+                    uint32_t v[U];
+#pragma unroll
+                    for (uint32_t u = 0; u < U; ++u) {
+                        const uint32_t j = lane + 64u * u;
+                        v[u] = j < nw && q0 + j < E ? A[q0 + j] : 0u;
+                    }
+#pragma unroll
+                    for (uint32_t u = 0; u < U; ++u) {
+                        const uint32_t j = lane + 64u * u;
+                        if (j < nwords) S[j] = q0 + j == E - 1 ? v[u] & tailm : v[u];
+                    }
+                }
                 if (lane == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 __builtin_amdgcn_wave_barrier();
                 asm volatile("" ::: "memory");
                 // LDS bit of payload bit b: b + bias; payload bits end at lim
                 // (and never past the staged words)
                 const uint32_t bias = 8 * s - 32 * q0;
-                const uint32_t lim0 = 8 * (s + len) - 32 * q0, slim = 32 * (nwords - 2);
+                const uint32_t lim0 = 8 * (s + len) - 32 * q0, slim = 32 * (nw - 2);
                 const uint32_t lim = lim0 < slim ? lim0 : slim;
                 const LdsBits Lb{S};
+                BP_DIAG(__builtin_amdgcn_s_waitcnt(0); const uint64_t t1 = __builtin_amdgcn_s_memtime());
                 const uint32_t b0 = 8 * k * st.R;                                     // region's first payload bit
                 const uint32_t b1 = 8 * (k + 1) * st.R < 8 * len ? 8 * (k + 1) * st.R : 8 * len;   // past its last
                 // 1. stored blocks, by their LEN / NLEN fields (a byte search
@@ -403,10 +452,18 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
                         break;
                     }
                 }
+                BP_DIAG(const uint64_t t2 = __builtin_amdgcn_s_memtime();
+                        if (lane == 0) {
+                            atomicAdd(&g_bp_diag[4], 1ull);
+                            atomicAdd(&g_bp_diag[8], t1 - t0);
+                            atomicAdd(&g_bp_diag[9], t2 - t1);
+                        })
                 if (best != 0xffffffffu) {
                     bit = best;
                     kind = KIND_STORED;
+                    BP_DIAG(if (lane == 0) atomicAdd(&g_bp_diag[5], 1ull));
                 } else {
+                    BP_DIAG(if (lane == 0) atomicAdd(&g_bp_diag[6], 1ull));
                     // 2. dynamic headers: block type 2, HLIT / HDIST in range
                     // and a complete code-length code (Kraft sum, table), in
                     // chunks; then the full check, one candidate per lane
@@ -451,6 +508,7 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
                         asm volatile("" ::: "memory");
                         const uint32_t c0 = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         const uint32_t nc = c0 < LIST ? c0 : LIST;
+                        BP_DIAG(if (lane == 0) atomicAdd(&g_bp_diag[7], (unsigned long long)nc));
                         asm volatile("" ::: "memory");
                         if (lane == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         asm volatile("" ::: "memory");
@@ -472,6 +530,7 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
                         bit = best;
                         kind = KIND_DYN;
                     }
+                    BP_DIAG(if (lane == 0) atomicAdd(&g_bp_diag[10], __builtin_amdgcn_s_memtime() - t2));
                 }
                 __builtin_amdgcn_wave_barrier();
             }
@@ -540,9 +599,7 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
 // ---------------------------------------------------------------- resolve
 typedef uint32_t uint32_ua __attribute__((aligned(1)));
 
-// diagnostics (bpmd_diag_bp_counters): payloads resolved, segments on their
-// chains, payloads sent to the wave kernel
-__device__ unsigned long long g_bp_diag[4];
+
 typedef uint2 uint2_sa __attribute__((aligned(2)));
 
 __global__ void __launch_bounds__(256)
@@ -773,15 +830,14 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
                                               nullptr, fb, q + 2, s);
 }
 
-// diagnostics: out[0] payloads resolved, out[1] segments on their chains,
-// out[2] fallbacks to the wave kernel; reset after reading
+// diagnostics: the 12 counters of g_bp_diag (out[12]); reset after reading
 extern "C" int bpmd_diag_bp_counters(unsigned long long* out, int reset)
 {
-    unsigned long long v[4] = {0, 0, 0, 0};
+    unsigned long long v[12] = {};
     if (hipMemcpyFromSymbol(v, HIP_SYMBOL(bpmd::bp::g_bp_diag), sizeof v) != hipSuccess) return -1;
-    for (int i = 0; i < 4; ++i) out[i] = v[i];
+    for (int i = 0; i < 12; ++i) out[i] = v[i];
     if (reset) {
-        const unsigned long long z[4] = {0, 0, 0, 0};
+        const unsigned long long z[12] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(bpmd::bp::g_bp_diag), z, sizeof z) != hipSuccess) return -1;
     }
     return 0;

@@ -25,7 +25,7 @@ def run(kind, n, size, producer, level, modes):
     torch.cuda.synchronize()
     comp = pmd.Batch(d.out.data, d.out.off, d.out.len)
     L = pmd.lib()
-    c0 = (ctypes.c_ulonglong * 4)()
+    c0 = (ctypes.c_ulonglong * 12)()
     L.bpmd_diag_bp_counters(c0, 1)
     for name in modes:
         L.bpmd_set_inflate_kernel(MODES[name])
@@ -40,12 +40,14 @@ def run(kind, n, size, producer, level, modes):
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
         t = float(np.median(ts))
-        c = (ctypes.c_ulonglong * 4)()
+        c = (ctypes.c_ulonglong * 12)()
         L.bpmd_diag_bp_counters(c, 1)
         runs = 6
         print(f"{kind:6s} {producer:5s} L{level} n={n:6d} size={size:6d} {name:5s} {t * 1e3:8.3f} ms "
               f"{n * size / t / 2**30:7.2f} GiB/s ok={ok}  bp: msgs {c[0] // runs} segs/msg "
-              f"{c[1] / max(c[0], 1):.1f} fallbacks {c[2] // runs}", flush=True)
+              f"{c[1] / max(c[0], 1):.1f} fallbacks {c[2] // runs} regions {c[4] // runs} stored {c[5] // runs} "
+              f"dynscan {c[6] // runs} deep {c[7] // runs} cyc/region stage {c[8] / max(c[4], 1):.0f} "
+              f"stored {c[9] / max(c[4], 1):.0f} dyn {c[10] / max(c[6], 1):.0f}", flush=True)
     L.bpmd_set_inflate_kernel(0)
 
 
