@@ -6,7 +6,8 @@ names).  So the kernel trace and the FETCH_SIZE / WRITE_SIZE passes of this
 process are the op's own.
 
     python scripts/leg_profile.py --leg c4_l6 --op inflate --steps 5
-legs: c3 (deflate only), c4_l6, c5_l1, c5_l6
+legs: c3 (deflate only), c4_l6, c5_l1, c5_l6; a suffix _s8 takes shard 0 of
+the byte-balanced 8-way split (what one rank of an 8-GPU node runs)
 """
 import argparse
 import os
@@ -27,19 +28,25 @@ LEGS = {"c4_l6": ("json", None, bench.SEED_C4, 6), "c5_l1": ("binary", 65536, be
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--leg", required=True, choices=sorted(LEGS))
+    ap.add_argument("--leg", required=True, choices=sorted(LEGS) + [k + "_s8" for k in LEGS if k != "c3"])
     ap.add_argument("--op", required=True, choices=["deflate", "inflate"])
     ap.add_argument("--steps", type=int, default=5)
     a = ap.parse_args()
-    kind, size, seed, level = LEGS[a.leg]
-    if a.leg == "c4_l6":
+    base = a.leg[:-3] if a.leg.endswith("_s8") else a.leg
+    kind, size, seed, level = LEGS[base]
+    first = 0
+    if base == "c4_l6":
         lens = synth.zipf_sizes(bench.C4_MSGS, seed)
     elif a.leg == "c3":
         lens = np.full(bench.N_MSGS, size, dtype=np.uint32)
     else:
         lens = np.full(bench.C5_MSGS, size, dtype=np.uint32)
+    if a.leg.endswith("_s8"):
+        from beast_amd import shard
+        first, e = shard.byte_balanced_ranges(lens, 8)[0]
+        lens = lens[first:e]
     dev = torch.device("cuda", 0)
-    raw, off, ln = synth.make_batch(kind, lens, seed=seed)
+    raw, off, ln = synth.make_batch(kind, lens, seed=seed, first=first)
     src = pmd.Batch(torch.from_numpy(raw).to(dev), torch.from_numpy(off.astype(np.int64)).to(dev),
                     torch.from_numpy(ln.astype(np.int32)).to(dev))
     del raw
@@ -65,11 +72,18 @@ def main():
     def inflate():
         return pmd.inflate_batch(comp, src.len, out=rbuf, out_off=src.off)
 
+    import ctypes
+    L = pmd.lib()
+    c = (ctypes.c_ulonglong * 12)()
+    L.bpmd_diag_bp_counters(c, 1)
     r = inflate()
     for _ in range(a.steps):
         inflate()
     torch.cuda.synchronize()
-    print("inflate steps", a.steps, "status_ok", int((r.status != 0).sum()) == 0)
+    L.bpmd_diag_bp_counters(c, 1)
+    runs = a.steps + 1
+    print(a.leg, "inflate steps", a.steps, "status_ok", int((r.status != 0).sum()) == 0, "msgs", len(lens),
+          "bp payloads/run", c[0] // runs, "segments/run", c[1] // runs, "wave fallbacks/run", c[2] / runs)
 
 
 if __name__ == "__main__":
