@@ -31,7 +31,8 @@ extern "C" int bpmd_internal_inflate_lane3(const uint8_t* in, const uint64_t* in
 extern "C" const uint32_t* bpmd_internal_lane_order(const uint32_t* in_len, uint32_t n, hipStream_t stream,
                                                     const uint32_t** keys_out);
 extern "C" const uint32_t* bpmd_internal_lane_long_split(const uint32_t* in_len, const uint32_t* keys, uint32_t n,
-                                                         uint32_t lanes, uint32_t min_thr, hipStream_t stream);
+                                                         uint32_t lanes, uint32_t min_thr, uint32_t share_pct,
+                                                         hipStream_t stream);
 extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n,
                                         uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                                         uint32_t* out_len, int32_t* status, uint32_t raw, const uint32_t* order,
@@ -88,9 +89,42 @@ struct StreamLock {
     hipStream_t stream;
     std::mutex* mu;
 };
+// A side stream per (device, stream): the long payloads of a work-queue
+// batch decode block-parallel on it while the lane kernel runs the rest on
+// the caller's stream (fork / join events; the caller's stream waits for the
+// side stream before anything after the batch call).
+struct Side {
+    int dev;
+    hipStream_t stream;
+    hipStream_t side;
+    hipEvent_t fork, join;
+};
 std::mutex g_scratch_mu;
 std::vector<Scratch> g_scratch;
 std::vector<StreamLock> g_locks;
+std::vector<Side> g_sides;
+
+bool side_for(hipStream_t s, Side& out)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    for (auto& e : g_sides)
+        if (e.dev == dev && e.stream == s) {
+            out = e;
+            return true;
+        }
+    Side d{dev, s, nullptr, nullptr, nullptr};
+    if (hipStreamCreateWithFlags(&d.side, hipStreamNonBlocking) != hipSuccess) return false;
+    if (hipEventCreateWithFlags(&d.fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&d.join, hipEventDisableTiming) != hipSuccess) {
+        (void)hipStreamDestroy(d.side);
+        return false;
+    }
+    g_sides.push_back(d);
+    out = d;
+    return true;
+}
 
 std::mutex* stream_mutex(hipStream_t s)
 {
@@ -159,8 +193,19 @@ extern "C" void bpmd_internal_scratch_release(hipStream_t s)
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return;
     std::lock_guard<std::mutex> lk(g_scratch_mu);
+    hipStream_t side = nullptr;
+    for (size_t i = 0; i < g_sides.size(); ++i)
+        if (g_sides[i].dev == dev && g_sides[i].stream == s) {
+            side = g_sides[i].side;
+            (void)hipStreamSynchronize(side);
+            (void)hipEventDestroy(g_sides[i].fork);
+            (void)hipEventDestroy(g_sides[i].join);
+            g_sides[i] = g_sides.back();
+            g_sides.pop_back();
+            break;
+        }
     for (size_t i = 0; i < g_scratch.size();) {
-        if (g_scratch[i].dev == dev && g_scratch[i].stream == s) {
+        if (g_scratch[i].dev == dev && (g_scratch[i].stream == s || (side && g_scratch[i].stream == side))) {
             (void)hipFree(g_scratch[i].p);
             g_scratch[i] = g_scratch.back();
             g_scratch.pop_back();
@@ -175,6 +220,7 @@ extern "C" void bpmd_internal_scratch_release(hipStream_t s)
             g_locks.pop_back();
             break;
         }
+    if (side) (void)hipStreamDestroy(side);
 }
 
 // Number of scratch blocks held (footprint tests)
@@ -288,7 +334,7 @@ int inflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
         // forced (tests): every payload of 64 bytes or more, the rest on lanes
         const uint32_t* keys = nullptr;
         const uint32_t* order = bpmd_internal_lane_order(d_in_len, n_msgs, s, &keys);
-        const uint32_t* nlong = order ? bpmd_internal_lane_long_split(d_in_len, keys, n_msgs, 0u, 64u, s) : nullptr;
+        const uint32_t* nlong = order ? bpmd_internal_lane_long_split(d_in_len, keys, n_msgs, 0u, 64u, 0u, s) : nullptr;
         if (!nlong || bpmd_internal_inflate_bp(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap,
                                                d_out_len, d_status, raw, order, nlong, s) ||
             bpmd_internal_inflate_lane3(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
@@ -339,12 +385,43 @@ int inflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
             if (ordered && !(order = bpmd_internal_lane_order(d_in_len, n_msgs, s, &keys))) return BPMD_R_HIP_ERROR;
             if (ordered && long_split && m == 0 && !hist) {
                 // long payloads: block-parallel, or one wave each
-                if (!(nlong = bpmd_internal_lane_long_split(d_in_len, keys, n_msgs, wgs * 64u, 4096u, s)) ||
-                    (bp_ok ? bpmd_internal_inflate_bp(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap,
-                                                      d_out_len, d_status, raw, order, nlong, s)
-                           : bpmd_internal_inflate_wave_ordered(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off,
-                                                                d_out_cap, d_out_len, d_status, raw, key, order,
-                                                                nlong, s)))
+                // (block-parallel: above half a lane's share of the batch, from
+                // 2 KiB compressed)
+                static const uint32_t share_pct = [] {
+                    const char* e = getenv("BPMD_LONG_SHARE_PCT");
+                    return e ? (uint32_t)strtoul(e, nullptr, 10) : 50u;
+                }();
+                if (!(nlong = bp_ok ? bpmd_internal_lane_long_split(d_in_len, keys, n_msgs, wgs * 64u, 2048u, share_pct, s)
+                                    : bpmd_internal_lane_long_split(d_in_len, keys, n_msgs, wgs * 64u, 4096u, 200u, s)))
+                    return BPMD_R_HIP_ERROR;
+                if (bp_ok) {
+                    // the lane kernel on the caller's stream (it skips the long
+                    // prefix of the order) and the long payloads block-parallel
+                    // on the side stream at the same time: each fills the CUs
+                    // the other's tail leaves idle
+                    Side sd;
+                    if (!side_for(s, sd) || hipEventRecord(sd.fork, s) != hipSuccess ||
+                        hipStreamWaitEvent(sd.side, sd.fork, 0) != hipSuccess)
+                        return BPMD_R_HIP_ERROR;
+                    static const bool bp_first = [] {
+                        const char* e = getenv("BPMD_BP_FIRST");
+                        return e && e[0] == '1';
+                    }();
+                    auto lane_part = [&] {
+                        return bpmd_internal_inflate_lane3(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off,
+                                                           d_out_cap, d_out_len, d_status, raw, key, hist,
+                                                           1u << cfg->window_bits, 0u, order, qctr, wgs, nlong, s);
+                    };
+                    if (!bp_first) e = lane_part();
+                    const int eb = bpmd_internal_inflate_bp(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off,
+                                                            d_out_cap, d_out_len, d_status, raw, order, nlong, sd.side);
+                    if (bp_first) e = lane_part();
+                    if (hipEventRecord(sd.join, sd.side) != hipSuccess || hipStreamWaitEvent(s, sd.join, 0) != hipSuccess)
+                        return BPMD_R_HIP_ERROR;
+                    return e || eb ? BPMD_R_HIP_ERROR : BPMD_R_OK;
+                }
+                if (bpmd_internal_inflate_wave_ordered(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap,
+                                                       d_out_len, d_status, raw, key, order, nlong, s))
                     return BPMD_R_HIP_ERROR;
             }
         } else if (split && bp_ok) {
@@ -352,7 +429,7 @@ int inflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
             // the same longest-first order after them
             const uint32_t* keys = nullptr;
             if (!(order = bpmd_internal_lane_order(d_in_len, n_msgs, s, &keys)) ||
-                !(nlong = bpmd_internal_lane_long_split(d_in_len, keys, n_msgs, 0u, split, s)) ||
+                !(nlong = bpmd_internal_lane_long_split(d_in_len, keys, n_msgs, 0u, split, 0u, s)) ||
                 bpmd_internal_inflate_bp(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
                                          d_status, raw, order, nlong, s))
                 return BPMD_R_HIP_ERROR;

@@ -16,12 +16,12 @@
 //      count and symbol workspace; exclusive sums give every payload's first
 //      task and workspace offset; the totals come back to the host (one
 //      small read-back) to size the workspace;
-//   2. scan (bp_scan_kernel): one wave per payload; region k > 0 is searched
+//   2. scan (bp_scan_kernel): one wave per region; region k > 0 is searched
 //      from its first bit for the first bit offset that passes a cheap filter
 //      (block type 2, HLIT <= 29, HDIST <= 29, a complete code-length code by
 //      Kraft sum) and then the full header check above.  Region 0's
-//      candidate is the payload's first bit.  Each candidate gets a symbol
-//      slot sized by its compressed span;
+//      candidate is the payload's first bit.  Then (bp_slots_kernel) each
+//      candidate gets a symbol slot sized by its compressed span;
 //   3. decode (pmd_inflate_lane3.hip, segment mode): one lane per candidate
 //      from its header to the first block boundary that is the payload's
 //      next candidate, as 16-bit symbols (bp.h); candidates that are not
@@ -90,7 +90,7 @@ bp_sum_kernel(const uint32_t* __restrict__ in_len, const uint32_t* __restrict__ 
 __global__ void __launch_bounds__(256)
 bp_stats_kernel(const uint32_t* __restrict__ in_len, const uint32_t* __restrict__ out_cap,
                 const uint32_t* __restrict__ order, const uint32_t* __restrict__ nlong, uint32_t n,
-                const unsigned long long* __restrict__ total, uint32_t lanes,
+                const unsigned long long* __restrict__ total, uint32_t lanes, uint32_t segs_per_lane,
                 Stat* __restrict__ st, uint32_t* __restrict__ regions, unsigned long long* __restrict__ words)
 {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
@@ -104,7 +104,7 @@ bp_stats_kernel(const uint32_t* __restrict__ in_len, const uint32_t* __restrict_
         // output per compressed byte the caller provisioned, capped at 4
         const uint64_t e16 = cap >= 4ull * len ? (4ull << 16) : (((uint64_t)cap << 16) / (len ? len : 1u));
         uint64_t R = cap ? ((uint64_t)SEG_OUT * len) / cap : R_MAX;
-        const uint64_t share = *total / (2ull * (lanes ? lanes : 1u));
+        const uint64_t share = *total / ((uint64_t)segs_per_lane * (lanes ? lanes : 1u));
         R = R < share ? share : R;
         R = R < R_MIN ? R_MIN : R > R_MAX ? R_MAX : R;
         R &= ~255ull;
@@ -357,12 +357,24 @@ struct ScanLds {
     uint32_t cnt[SCAN_WAVES];
 };
 
+// region -> long-list index, for the scan's per-region work items
+__global__ void __launch_bounds__(256)
+bp_region_map_kernel(const uint32_t* __restrict__ nlong, const uint32_t* __restrict__ regions,
+                     const uint32_t* __restrict__ task_base, uint32_t* __restrict__ map)
+{
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= *nlong) return;
+    const uint32_t tb = task_base[i], nr = regions[i];
+    for (uint32_t k = 0; k < nr; ++k) map[tb + k] = i;
+}
+
+// One wave per region (all regions of all long payloads in one index space,
+// so a batch of few payloads still spreads over the chip).
 __global__ void __launch_bounds__(64 * SCAN_WAVES)
 bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                const uint32_t* __restrict__ in_len, const uint32_t* __restrict__ order,
-               const uint32_t* __restrict__ nlong, const Stat* __restrict__ stats,
-               const uint32_t* __restrict__ task_base, const unsigned long long* __restrict__ word_base,
-               SegTask* __restrict__ tasks, uint32_t* __restrict__ qctr)
+               const uint32_t* __restrict__ region_map, uint32_t n_regions, const Stat* __restrict__ stats,
+               const uint32_t* __restrict__ task_base, SegTask* __restrict__ tasks)
 {
     __shared__ ScanLds L;
     for (uint32_t f = threadIdx.x; f < 4096; f += blockDim.x) L.kraft[f] = (uint16_t)kraft4(f);
@@ -371,12 +383,11 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
     uint32_t* S = L.stage[wv];
     uint32_t* list = L.list[wv];
     uint32_t* cnt = &L.cnt[wv];
-    const uint32_t end = *nlong;
-    for (;;) {
-        uint32_t i = 0;
-        if (lane == 0) i = atomicAdd(qctr, 1u);
-        i = (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
-        if (i >= end) break;
+    // static grid stride: regions cost about the same, and one counter
+    // taken per region serialises on its atomics (C5: 131 072 regions)
+    const uint32_t waves = gridDim.x * SCAN_WAVES;
+    for (uint32_t g = blockIdx.x * SCAN_WAVES + wv; g < n_regions; g += waves) {
+        const uint32_t i = (uint32_t)__builtin_amdgcn_readfirstlane((int)region_map[g]);
         const uint32_t m = order[i];
         const Stat st = stats[i];
         const uint32_t len = in_len[m];
@@ -386,7 +397,8 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
         const uint32_t* A = (const uint32_t*)(p - s);
         const uint32_t E = (s + len + 3) >> 2;   // dwords holding payload bytes
         const GlobalBits G{A, E};
-        for (uint32_t k = 0; k < st.regions; ++k) {
+        {
+            const uint32_t k = g - tb;
             uint32_t bit = 0, kind = KIND_START;
             if (k) {
                 kind = KIND_NONE;
@@ -546,16 +558,31 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
                 tasks[tb + k] = t;
             }
         }
-        __builtin_amdgcn_s_waitcnt(0);
         __builtin_amdgcn_wave_barrier();
-        // slots: each candidate's span runs to the next candidate (or the end
-        // of the payload); slot = span x F16 + SLACK symbols, laid out in order
+    }
+}
+
+// Slots, one wave per long payload once every region is scanned: each
+// candidate's span runs to the next candidate (or the end of the payload);
+// slot = span x F16 + SLACK symbols, laid out in order.
+__global__ void __launch_bounds__(256)
+bp_slots_kernel(const uint32_t* __restrict__ in_len, const uint32_t* __restrict__ order,
+                const uint32_t* __restrict__ nlong, const Stat* __restrict__ stats,
+                const uint32_t* __restrict__ task_base, const unsigned long long* __restrict__ word_base,
+                SegTask* __restrict__ tasks)
+{
+    const uint32_t lane = wave_lane();
+    const uint32_t end = *nlong;
+    for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < end; i += (gridDim.x * blockDim.x) >> 6) {
+        const Stat st = stats[i];
+        const uint32_t len = in_len[order[i]];
+        const uint32_t tb = task_base[i];
         uint64_t run = word_base[i] + SYM_GUARD;
         uint32_t nextbit = 8 * len;   // the next candidate's bit, from the chunk after
         const uint32_t nch = (st.regions + 63) / 64;
         // chunks from the last to the first (suffix "next candidate" scan),
         // slot offsets assigned afterwards from the first
-        volatile SegTask* vt = tasks + tb;   // written above by lane 0: read past the L1
+        SegTask* vt = tasks + tb;
         for (uint32_t c = nch; c-- > 0;) {
             const uint32_t k = c * 64 + lane;
             const bool v = k < st.regions && vt[k].kind != KIND_NONE;
@@ -598,6 +625,7 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
 
 // ---------------------------------------------------------------- resolve
 typedef uint32_t uint32_ua __attribute__((aligned(1)));
+typedef uint4 uint4_ua __attribute__((aligned(1)));
 
 
 typedef uint2 uint2_sa __attribute__((aligned(2)));
@@ -635,20 +663,25 @@ bp_resolve_kernel(const uint32_t* __restrict__ order, const uint32_t* __restrict
             const uint32_t n = r.nsym;
             const uint32_t room = cap - P;   // P <= cap
             uint32_t bad = n;                // first symbol referring before the payload
-            for (uint32_t c = 0; c < n; c += 256) {
-                const uint32_t j0 = c + 4 * lane;
-                uint32_t v[4] = {0, 0, 0, 0};
-                if (j0 + 4 <= n) {
-                    const uint2 w = *(const uint2_sa*)(sy + j0);
-                    v[0] = w.x & 0xffffu; v[1] = w.x >> 16; v[2] = w.y & 0xffffu; v[3] = w.y >> 16;
+            // 16 symbols per lane per step, all loads in flight together
+            for (uint32_t c = 0; c < n; c += 1024) {
+                const uint32_t j0 = c + 16 * lane;
+                uint32_t v[16];
+                if (j0 + 16 <= n) {
+#pragma unroll
+                    for (int h = 0; h < 4; ++h) {
+                        const uint2 w = *(const uint2_sa*)(sy + j0 + 4 * h);
+                        v[4 * h] = w.x & 0xffffu; v[4 * h + 1] = w.x >> 16;
+                        v[4 * h + 2] = w.y & 0xffffu; v[4 * h + 3] = w.y >> 16;
+                    }
                 } else {
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) v[q] = j0 + q < n ? sy[j0 + q] : 0u;
+                    for (int q = 0; q < 16; ++q) v[q] = j0 + q < n ? sy[j0 + q] : 0u;
                 }
                 uint32_t lbad = 0xffffffffu;
-                uint32_t bytes[4];
+                uint32_t bytes[16];
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
+                for (int q = 0; q < 16; ++q) {
                     const uint32_t x = v[q];
                     bytes[q] = x & 0xffu;
                     if (j0 + q < n && (x & SYM_REF)) {
@@ -660,25 +693,29 @@ bp_resolve_kernel(const uint32_t* __restrict__ order, const uint32_t* __restrict
                         }
                     }
                 }
-                // the first invalid reference of the chunk (in stream order)
+                // the first invalid reference of the step (in stream order)
                 uint32_t mb = lbad;
                 for (uint32_t d = 32; d >= 1; d >>= 1) {
                     const uint32_t y = __shfl_xor(mb, d);
                     mb = y < mb ? y : mb;
                 }
                 const uint32_t upto = (mb < n ? mb : n) < room ? (mb < n ? mb : n) : room;
-                if (j0 + 4 <= upto) {
-                    *(uint32_ua*)(o + P + j0) = bytes[0] | (bytes[1] << 8) | (bytes[2] << 16) | (bytes[3] << 24);
+                if (j0 + 16 <= upto) {
+                    uint32_t d4[4];
+#pragma unroll
+                    for (int h = 0; h < 4; ++h)
+                        d4[h] = bytes[4 * h] | (bytes[4 * h + 1] << 8) | (bytes[4 * h + 2] << 16) | (bytes[4 * h + 3] << 24);
+                    *(uint4_ua*)(o + P + j0) = make_uint4(d4[0], d4[1], d4[2], d4[3]);
                 } else {
 #pragma unroll
-                    for (int q = 0; q < 4; ++q)
+                    for (int q = 0; q < 16; ++q)
                         if (j0 + q < upto) o[P + j0 + q] = (uint8_t)bytes[q];
                 }
                 if (mb != 0xffffffffu) {
                     bad = mb;
                     break;
                 }
-                if (c + 256 > room) break;   // the rest lies past the capacity
+                if (c + 1024 > room) break;   // the rest lies past the capacity
             }
             if (bad < n) {
                 // the token at P + bad has a distance past the output so far
@@ -789,8 +826,14 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
     if (hipMemsetAsync(q, 0, 64, s) != hipSuccess) return (int)hipErrorUnknown;
     hipLaunchKernelGGL(bp_sum_kernel, dim3(n / 256 + 1 < 1024 ? n / 256 + 1 : 1024), dim3(256), 0, s, in_len, order,
                        nlong, n, total);
+    // BPMD_BP_SEGS (diagnostics): target segments per lane of the chip
+    static const uint32_t segs = [] {
+        const char* e = getenv("BPMD_BP_SEGS");
+        const uint32_t v = e ? (uint32_t)strtoul(e, nullptr, 10) : 0u;
+        return v ? v : 2u;
+    }();
     hipLaunchKernelGGL(bp_stats_kernel, dim3((n + 255) / 256), dim3(256), 0, s, in_len, out_cap, order, nlong, n, total,
-                       256u * (uint32_t)cus, st, reg, words);
+                       256u * (uint32_t)cus, segs, st, reg, words);
     if (hipGetLastError() != hipSuccess) return (int)hipErrorUnknown;
     size_t t1 = tmp1, t2 = tmp2;
     if (hipcub::DeviceScan::ExclusiveSum(tmp, t1, reg, tbase, (int)n, s) != hipSuccess ||
@@ -806,17 +849,23 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
     if (ntask > 0xffffffffull) return (int)hipErrorInvalidValue;
     // decode workspace (scratch block 11): tasks, results, fallback list, symbols
     const size_t d_tasks = 0, d_res = al256(d_tasks + sizeof(SegTask) * ntask), d_fb = al256(d_res + sizeof(SegRes) * ntask),
-                 d_sym = al256(d_fb + 4ull * n), dsz = al256(d_sym + 2ull * (nword + SYM_GUARD + 64));
+                 d_map = al256(d_fb + 4ull * n), d_sym = al256(d_map + 4ull * ntask),
+                 dsz = al256(d_sym + 2ull * (nword + SYM_GUARD + 64));
     uint8_t* dw = (uint8_t*)bpmd_internal_scratch(s, dsz, 11);
     if (!dw) return (int)hipErrorOutOfMemory;
     SegTask* tasks = (SegTask*)(dw + d_tasks);
     SegRes* res = (SegRes*)(dw + d_res);
     uint32_t* fb = (uint32_t*)(dw + d_fb);
     uint16_t* sym = (uint16_t*)(dw + d_sym);
-    // scan: SCAN_WAVES waves per workgroup, ~3 workgroups per CU by LDS
+    uint32_t* rmap = (uint32_t*)(dw + d_map);
+    // scan: one wave per region, SCAN_WAVES waves per workgroup, ~3
+    // workgroups per CU by LDS; then the slots, one wave per payload
+    hipLaunchKernelGGL(bp_region_map_kernel, dim3((n + 255) / 256), dim3(256), 0, s, nlong, reg, tbase, rmap);
     const uint32_t scan_wgs = 3u * (uint32_t)cus;
-    hipLaunchKernelGGL(bp_scan_kernel, dim3(scan_wgs), dim3(64 * SCAN_WAVES), 0, s, in, in_off, in_len, order, nlong,
-                       st, tbase, wbase, tasks, q + 0);
+    hipLaunchKernelGGL(bp_scan_kernel, dim3(scan_wgs), dim3(64 * SCAN_WAVES), 0, s, in, in_off, in_len, order, rmap,
+                       (uint32_t)ntask, st, tbase, tasks);
+    hipLaunchKernelGGL(bp_slots_kernel, dim3(4u * (uint32_t)cus), dim3(256), 0, s, in_len, order, nlong, st, tbase,
+                       wbase, tasks);
     if (hipGetLastError() != hipSuccess) return (int)hipErrorUnknown;
     const uint32_t wgs = 4u * (uint32_t)cus;
     int e = bpmd_internal_inflate_lane3_seg(in, in_off, in_len, (uint32_t)ntask, tasks, sym, res, raw,

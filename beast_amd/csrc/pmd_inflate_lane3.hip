@@ -1627,10 +1627,11 @@ extern "C" const uint32_t* bpmd_internal_lane_order(const uint32_t* in_len, uint
 // that alone takes longer than the whole batch's share per lane sets the
 // launch's end (at 8 GPUs, each rank's C4 shard ran ~20 ms on its 64 KiB
 // messages against ~5 ms for the rest).  Those payloads go to the wave
-// kernel, which decodes one message with 64 lanes.  "Longer than its share":
-// compressed length above 2x the batch's compressed bytes per resident lane,
-// and never below 4 KiB (the per-message split the two kernels were tuned
-// at).  The count is computed on the device from the sorted keys, so the
+// kernel, which decodes one message with 64 lanes, or to the block-parallel
+// decoder, which cuts it at block starts.  "Longer than its share":
+// compressed length above share_pct % of the batch's compressed bytes per
+// resident lane (block-parallel: 50 %, so the work queue ends near the
+// per-lane share; wave kernel: 200 %), and never below min_thr.  The count is computed on the device from the sorted keys, so the
 // call stays asynchronous: split[0] = total compressed bytes (u64),
 // split[2] = number of long payloads = a prefix of the longest-first order.
 namespace bpmd {
@@ -1644,7 +1645,7 @@ __global__ void __launch_bounds__(256) sum_in_kernel(const uint32_t* __restrict_
     if ((threadIdx.x & 63) == 0 && acc) atomicAdd(total, acc);
 }
 __global__ void long_count_kernel(const uint32_t* __restrict__ keys, uint32_t n, uint32_t lanes, uint32_t min_thr,
-                                  unsigned long long* __restrict__ split)
+                                  uint32_t share_pct, unsigned long long* __restrict__ split)
 {
     if (threadIdx.x != 0) return;
     if (min_thr == 0 && lanes == 0) {   // every payload
@@ -1652,7 +1653,7 @@ __global__ void long_count_kernel(const uint32_t* __restrict__ keys, uint32_t n,
         return;
     }
     const unsigned long long total = split[0];
-    unsigned long long thr = lanes ? 2ull * total / lanes : 0ull;
+    unsigned long long thr = lanes ? (unsigned long long)share_pct * total / (100ull * lanes) : 0ull;
     if (thr < min_thr) thr = min_thr;
     const uint32_t tk = (uint32_t)((thr + 63) >> 6);   // long: key > tk (keys descending)
     uint32_t lo = 0, hi = n;
@@ -1670,13 +1671,15 @@ __global__ void long_count_kernel(const uint32_t* __restrict__ keys, uint32_t n,
 // order bpmd_internal_lane_order returned with `keys`), or null on error.
 // lanes == 0: a fixed threshold of min_thr compressed bytes (0: every payload).
 extern "C" const uint32_t* bpmd_internal_lane_long_split(const uint32_t* in_len, const uint32_t* keys, uint32_t n,
-                                                         uint32_t lanes, uint32_t min_thr, hipStream_t stream)
+                                                         uint32_t lanes, uint32_t min_thr, uint32_t share_pct,
+                                                         hipStream_t stream)
 {
     unsigned long long* split = (unsigned long long*)bpmd_internal_scratch(stream, 256, 9);
     if (!split || hipMemsetAsync(split, 0, 16, stream) != hipSuccess) return nullptr;
     const uint32_t blocks = n / 256 + 1 < 1024 ? n / 256 + 1 : 1024;
     hipLaunchKernelGGL(bpmd::lp3::sum_in_kernel, dim3(blocks), dim3(256), 0, stream, in_len, n, split);
-    hipLaunchKernelGGL(bpmd::lp3::long_count_kernel, dim3(1), dim3(64), 0, stream, keys, n, lanes, min_thr, split);
+    hipLaunchKernelGGL(bpmd::lp3::long_count_kernel, dim3(1), dim3(64), 0, stream, keys, n, lanes, min_thr, share_pct,
+                       split);
     if (hipGetLastError() != hipSuccess) return nullptr;
     return (const uint32_t*)split + 2;
 }

@@ -20,12 +20,13 @@ def main():
             short = name.split("(")[0].replace("void ", "")
             d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
             per.setdefault(short, []).append((int(r["Start_Timestamp"]), d))
-    print("kernel,calls,median_ns_warm,mean_ns_all,min_ns,max_ns,first_ns")
+    w = csv.writer(sys.stdout, lineterminator="\n")   # kernel names hold commas: quoted
+    w.writerow(["kernel", "calls", "median_ns_warm", "mean_ns_all", "min_ns", "max_ns", "first_ns"])
     for k, v in sorted(per.items(), key=lambda kv: -sum(d for _, d in kv[1])):
         v.sort()
         ds = [d for _, d in v]
         warm = ds[1:] if len(ds) > 1 else ds
-        print(f"{k},{len(ds)},{int(statistics.median(warm))},{int(statistics.mean(ds))},{min(ds)},{max(ds)},{ds[0]}")
+        w.writerow([k, len(ds), int(statistics.median(warm)), int(statistics.mean(ds)), min(ds), max(ds), ds[0]])
 
 
 if __name__ == "__main__":
