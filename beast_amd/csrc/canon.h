@@ -21,13 +21,13 @@ struct Canon {
 template <int NB>
 __device__ __forceinline__ uint32_t canon_min(const uint32_t (&Q)[NB], uint32_t c)
 {
+    // a chain of three-input mins (v_min3_u32): NB - 1 values fold in
+    // (NB - 1) / 2 instructions
     const uint32_t k1 = (c + 1) << 15;
     uint32_t m = Q[0] - k1;
 #pragma unroll
-    for (int i = 1; i + 1 < NB; i += 2) {
-        const uint32_t x = Q[i] - k1, y = Q[i + 1] - k1;
-        m = __builtin_elementwise_min(m, __builtin_elementwise_min(x, y));
-    }
+    for (int i = 1; i + 1 < NB; i += 2)
+        m = __builtin_elementwise_min(__builtin_elementwise_min(m, Q[i] - k1), Q[i + 1] - k1);
     if (NB % 2 == 0) m = __builtin_elementwise_min(m, Q[NB - 1] - k1);
     return m;
 }
