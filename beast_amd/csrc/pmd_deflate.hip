@@ -737,7 +737,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
                 const unsigned q = g + lane;
                 uint32_t pv = NONE;
                 if (q + MIN_MATCH <= wn) {
-                    const uint32_t h = hash3(W.dw(q), HB);
+                    const uint32_t h = chain_hash(W.dw(q), wn - q, HB);
                     const uint32_t pre = S.b.head[h];
                     const uint32_t old = atomicExch(&S.b.head[h], q);
                     const uint32_t c = old < q ? old : pre;

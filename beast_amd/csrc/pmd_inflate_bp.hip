@@ -789,12 +789,26 @@ BpHost& bp_host()
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 }  // namespace
 
-extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n,
-                                        uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
-                                        uint32_t* out_len, int32_t* status, uint32_t raw, const uint32_t* order,
-                                        const uint32_t* nlong, hipStream_t s)
+// Phase 1 (plan): per-payload stats, the exclusive sums and one small
+// read-back of the totals to size the decode workspace; the host waits for
+// it, so a caller that overlaps other work launches that work after this.
+// Phase 2 (run): scan, slots, segment decode, resolve, fallback.  Both on s.
+struct BpPlan {
+    uint32_t n, cus;
+    uint64_t ntask, nword;
+    bpmd::bp::Stat* st;
+    uint32_t *reg, *tbase, *q;
+    unsigned long long* wbase;
+};
+thread_local BpPlan g_plan;
+
+extern "C" int bpmd_internal_inflate_bp_plan(const uint32_t* in_len, uint32_t n, const uint32_t* out_cap,
+                                             const uint32_t* order, const uint32_t* nlong, hipStream_t s,
+                                             uint64_t* ntask_out)
 {
     using namespace bpmd::bp;
+    *ntask_out = 0;
+    g_plan.ntask = 0;
     if (n == 0) return 0;
     BpHost& H = bp_host();
     if (!H.tot || !H.ev) return (int)hipErrorOutOfMemory;
@@ -818,7 +832,7 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
     unsigned long long* words = (unsigned long long*)(ws + o_w);
     unsigned long long* wbase = (unsigned long long*)(ws + o_wb);
     Totals* dtot = (Totals*)(ws + o_tot);
-    uint32_t* q = (uint32_t*)(ws + o_q);   // [0] scan queue, [1] resolve queue, [2] fallback count, [3] seg queue
+    uint32_t* q = (uint32_t*)(ws + o_q);
     void* tmp = ws + o_tmp;
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -844,9 +858,25 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
         hipMemcpyAsync(H.tot, dtot, sizeof(Totals), hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipEventRecord(H.ev, s) != hipSuccess || hipEventSynchronize(H.ev) != hipSuccess)
         return (int)hipErrorUnknown;
-    const uint64_t ntask = H.tot->tasks, nword = H.tot->words;
+    if (H.tot->tasks > 0xffffffffull) return (int)hipErrorInvalidValue;
+    g_plan = BpPlan{n, (uint32_t)cus, H.tot->tasks, H.tot->words, st, reg, tbase, q, wbase};
+    *ntask_out = H.tot->tasks;
+    return 0;
+}
+
+extern "C" int bpmd_internal_inflate_bp_run(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                            uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                                            uint32_t* out_len, int32_t* status, uint32_t raw, const uint32_t* order,
+                                            const uint32_t* nlong, hipStream_t s)
+{
+    using namespace bpmd::bp;
+    const BpPlan P = g_plan;
+    const uint64_t ntask = P.ntask, nword = P.nword;
     if (ntask == 0) return 0;
-    if (ntask > 0xffffffffull) return (int)hipErrorInvalidValue;
+    const uint32_t n = P.n, cus = P.cus;
+    Stat* st = P.st;
+    uint32_t *reg = P.reg, *tbase = P.tbase, *q = P.q;
+    unsigned long long* wbase = P.wbase;
     // decode workspace (scratch block 11): tasks, results, fallback list, symbols
     const size_t d_tasks = 0, d_res = al256(d_tasks + sizeof(SegTask) * ntask), d_fb = al256(d_res + sizeof(SegRes) * ntask),
                  d_map = al256(d_fb + 4ull * n), d_sym = al256(d_map + 4ull * ntask),
@@ -861,22 +891,35 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
     // scan: one wave per region, SCAN_WAVES waves per workgroup, ~3
     // workgroups per CU by LDS; then the slots, one wave per payload
     hipLaunchKernelGGL(bp_region_map_kernel, dim3((n + 255) / 256), dim3(256), 0, s, nlong, reg, tbase, rmap);
-    const uint32_t scan_wgs = 3u * (uint32_t)cus;
+    const uint32_t scan_wgs = 3u * cus;
     hipLaunchKernelGGL(bp_scan_kernel, dim3(scan_wgs), dim3(64 * SCAN_WAVES), 0, s, in, in_off, in_len, order, rmap,
                        (uint32_t)ntask, st, tbase, tasks);
-    hipLaunchKernelGGL(bp_slots_kernel, dim3(4u * (uint32_t)cus), dim3(256), 0, s, in_len, order, nlong, st, tbase,
+    hipLaunchKernelGGL(bp_slots_kernel, dim3(4u * cus), dim3(256), 0, s, in_len, order, nlong, st, tbase,
                        wbase, tasks);
     if (hipGetLastError() != hipSuccess) return (int)hipErrorUnknown;
-    const uint32_t wgs = 4u * (uint32_t)cus;
+    const uint32_t wgs = 4u * cus;
     int e = bpmd_internal_inflate_lane3_seg(in, in_off, in_len, (uint32_t)ntask, tasks, sym, res, raw,
                                             (uint64_t)ntask > (uint64_t)wgs * 64u ? q + 3 : nullptr, wgs, s);
     if (e) return e;
-    hipLaunchKernelGGL(bp_resolve_kernel, dim3(8u * (uint32_t)cus), dim3(256), 0, s, order, nlong, tbase, tasks, res,
+    hipLaunchKernelGGL(bp_resolve_kernel, dim3(8u * cus), dim3(256), 0, s, order, nlong, tbase, tasks, res,
                        sym, out, out_off, out_cap, out_len, status, raw, fb, q + 2, q + 1, st);
     if (hipGetLastError() != hipSuccess) return (int)hipErrorUnknown;
     // payloads whose output outgrew the slots: the wave kernel, from the list
     return bpmd_internal_inflate_wave_ordered(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, raw,
                                               nullptr, fb, q + 2, s);
+}
+
+
+extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n,
+                                        uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                                        uint32_t* out_len, int32_t* status, uint32_t raw, const uint32_t* order,
+                                        const uint32_t* nlong, hipStream_t s)
+{
+    uint64_t ntask = 0;
+    const int e = bpmd_internal_inflate_bp_plan(in_len, n, out_cap, order, nlong, s, &ntask);
+    if (e || ntask == 0) return e;
+    return bpmd_internal_inflate_bp_run(in, in_off, in_len, out, out_off, out_cap, out_len, status, raw, order, nlong,
+                                        s);
 }
 
 // diagnostics: the 12 counters of g_bp_diag (out[12]); reset after reading

@@ -206,8 +206,8 @@ def pmc_traffic(kernel):
 # the number of steps in the PMC pass)
 LEG_ANCHOR = {("c3", "deflate"): "deflate_kernel", ("c4_l6", "deflate"): "stitch_kernel",
               ("c4_l6", "inflate"): "inflate_lane3_kernel", ("c5_l1", "deflate"): "stitch_kernel",
-              ("c5_l1", "inflate"): "inflate_kernel", ("c5_l6", "deflate"): "stitch_kernel",
-              ("c5_l6", "inflate"): "inflate_kernel"}
+              ("c5_l1", "inflate"): "inflate_lane3_seg_kernel", ("c5_l6", "deflate"): "stitch_kernel",
+              ("c5_l6", "inflate"): "inflate_lane3_seg_kernel"}
 
 
 def pmc_traffic_leg(leg, op):
@@ -224,6 +224,8 @@ def pmc_traffic_leg(leg, op):
     with open(f) as fh:
         for r in csv.DictReader(fh):
             k = r["kernel"].split("::")[-1].split("<")[0]
+            if op == "inflate" and "dfl::" in r["kernel"]:
+                continue   # the one setup deflate of scripts/leg_profile.py
             v = float(r["value_kB"]) * 1024
             if r["counter"] == "FETCH_SIZE":
                 fetch += v
@@ -304,8 +306,13 @@ def roofline(alg_bytes, kern_ms, kernels, traffic=None):
 
 
 DEFLATE_STEP_KERNELS = "deflate_kernel + count_chunks + scan + fill_items + deflate_chunks + stitch"
-INFLATE_STEP_KERNELS = {"c4_l6": "order_keys + radix sort + inflate_lane3_kernel (work queue)",
-                        "c5_l1": "inflate_kernel (wave per message)", "c5_l6": "inflate_kernel (wave per message)"}
+INFLATE_STEP_KERNELS = {
+    "c4_l6": "order_keys + radix sort + inflate_lane3_kernel (work queue; at N >= 2 the long payloads "
+             "block-parallel on a side stream: bp_scan + inflate_lane3_seg_kernel + bp_resolve)",
+    "c5_l1": "order_keys + radix sort + bp_stats + bp_scan + bp_slots + inflate_lane3_seg_kernel + bp_resolve "
+             "(block-parallel)",
+    "c5_l6": "order_keys + radix sort + bp_stats + bp_scan + bp_slots + inflate_lane3_seg_kernel + bp_resolve "
+             "(block-parallel)"}
 
 
 def mixed_legs(args, rank, world, timer, dev):

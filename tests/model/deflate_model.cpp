@@ -165,8 +165,8 @@ static std::vector<uint8_t> encode(const uint8_t* msg, unsigned n, const Params&
             prev.assign(wn, -1);
             std::fill(head.begin(), head.end(), -1);
             for (unsigned q = 0; q + MIN_MATCH <= wn; ++q) {
-                uint32_t x = w[q] | (w[q + 1] << 8) | (w[q + 2] << 16);
-                uint32_t h = hash3(x, P.hbits);
+                uint32_t x = w[q] | (w[q + 1] << 8) | (w[q + 2] << 16) | (q + 3 < wn ? (uint32_t)w[q + 3] << 24 : 0u);
+                uint32_t h = chain_hash(x, wn - q, P.hbits);
                 prev[q] = head[h];
                 head[h] = (int32_t)q;
             }
