@@ -50,10 +50,11 @@ LZ_HD Level level_params(int level)
 }
 
 // Chain limit the GPU encoder uses: the level table's, capped at
-// BPMD_CHAIN_CAP for messages of one 4 KiB chunk (C3 corpus at level 6, final
-// round-2 build with the message queue: cap 8 / 12 / 16 = 37.4 / 35.0 / 33.1
-// GiB/s at 1.038 / 1.028 / 1.020x Beast's size; 16 is the
-// default) and at BPMD_CHAIN_CAP_MULTI (0 = the table's value) for the chunks
+// BPMD_CHAIN_CAP for messages of one 4 KiB chunk (C3 corpus at level 6 with
+// 4-byte chain keys, round 3: cap 16 / 12 / 8 / 6 / 5 / 4 = 34.1 / 35.5 /
+// 37.6 / 39.5 / 40.3 / 41.2 GiB/s at 0.991 / 0.994 / 1.001 / 1.006 / 1.011 /
+// 1.016x Beast's size; 4 is the default: the fastest within
+// 1.02x) and at BPMD_CHAIN_CAP_MULTI (0 = the table's value) for the chunks
 // of longer messages, which see BPMD_CHUNK_HIST bytes of history before the
 // chunk.  configs[3] (C4), whole batch, size against Beast at level 6 and
 // deflate GiB/s:
@@ -61,7 +62,7 @@ LZ_HD Level level_params(int level)
 //   history 2048, cap 16: 1.111x, 23.9 (6 waves per CU)
 //   history 2048, cap 32: 1.089x, 20.9   <- default
 #ifndef BPMD_CHAIN_CAP
-#define BPMD_CHAIN_CAP 16
+#define BPMD_CHAIN_CAP 4
 #endif
 #ifndef BPMD_CHAIN_CAP_MULTI
 #define BPMD_CHAIN_CAP_MULTI 32
@@ -132,7 +133,12 @@ LZ_HD uint32_t reverse_bits(uint32_t code, unsigned len)
 // 33.1 -> 34.4 GiB/s, 1.020 -> 0.991x Beast's size.
 LZ_HD uint32_t chain_hash(uint32_t w, unsigned avail, unsigned hbits)
 {
+#ifdef BPMD_CHAIN_KEY3   // diagnostics: round 2's 3-byte keys
+    (void)avail;
+    return ((w & 0xFFFFFFu) * 0x9E3779B1u) >> (32 - hbits);
+#else
     return ((avail >= 4 ? w : (w & 0xFFFFFFu)) * 0x9E3779B1u) >> (32 - hbits);
+#endif
 }
 
 // ---------------------------------------------------------------- Huffman

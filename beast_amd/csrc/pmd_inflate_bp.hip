@@ -336,8 +336,17 @@ __device__ bool stored_ok(const GlobalBits& G, const LdsBits& Lb, uint32_t bias,
     const bool staged = lq + 96 <= lim;
     const uint32_t h = staged ? Lb.peek(lq) : G.peek(8 * (s + q));
     const uint32_t type = (h >> 1) & 3u;
-    if (type == 2)
-        return staged ? dyn_header_quick(Lb, lq, lim) : dyn_header_quick(G, 8 * (s + q), 8 * (s + len));
+    // a dynamic header after it.  The quick filter passes ~1 in 4 000 random
+    // offsets, which let about one false stored candidate per GiB of
+    // near-random payload through (LEN / NLEN match 1 in 65 536 positions),
+    // and a false candidate before a region's real one sizes the real
+    // segment's slot short (the payload then falls back to the wave kernel).
+    // An empty block (a sync marker, 00 00 FF FF: 1 in 2^32) keeps the quick
+    // filter; any other length also passes the full header check.
+    if (type == 2) {
+        const bool quick = staged ? dyn_header_quick(Lb, lq, lim) : dyn_header_quick(G, 8 * (s + q), 8 * (s + len));
+        return quick && (L == 0 || dyn_header_ok(G, 8 * (s + q), 8 * (s + len)));
+    }
     if (type == 0) {
         if (q + 5 > len) return false;
         const uint32_t w = staged && lq + 8 + 32 <= lim ? Lb.peek(lq + 8) : G.peek(8 * (s + q + 1));

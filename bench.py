@@ -187,7 +187,10 @@ def pmc_traffic(kernel):
         for r in csv.DictReader(fh):
             if r["kernel"].split("::")[-1].split("<")[0] != kernel:
                 continue
-            (fetch if r["counter"] == "FETCH_SIZE" else write).append(float(r["value_kB"]) * 1024)
+            try:
+                (fetch if r["counter"] == "FETCH_SIZE" else write).append(float(r["value_kB"]) * 1024)
+            except (TypeError, ValueError):
+                continue
     if not fetch or not write:
         return None, None
     factor, calib = 1.0, None
@@ -226,7 +229,10 @@ def pmc_traffic_leg(leg, op):
             k = r["kernel"].split("::")[-1].split("<")[0]
             if op == "inflate" and "dfl::" in r["kernel"]:
                 continue   # the one setup deflate of scripts/leg_profile.py
-            v = float(r["value_kB"]) * 1024
+            try:
+                v = float(r["value_kB"]) * 1024
+            except (TypeError, ValueError):
+                continue   # a malformed row (never a reason to lose the bench line)
             if r["counter"] == "FETCH_SIZE":
                 fetch += v
                 anchors += k == LEG_ANCHOR[(leg, op)]

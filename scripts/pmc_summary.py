@@ -9,7 +9,8 @@ import sys
 
 
 def main():
-    print("kernel,dispatch,counter,value_kB")
+    w = csv.writer(sys.stdout, lineterminator="\n")   # kernel names hold commas: quoted
+    w.writerow(["kernel", "dispatch", "counter", "value_kB"])
     for path in sys.argv[1:]:
         acc = {}
         with open(path) as f:
@@ -23,7 +24,7 @@ def main():
                 key = (short, r["Dispatch_Id"], r["Counter_Name"])
                 acc[key] = acc.get(key, 0.0) + float(r["Counter_Value"])
         for (k, d, c), v in sorted(acc.items(), key=lambda x: int(x[0][1])):
-            print(f"{k},{d},{c},{v:.6f}")
+            w.writerow([k, d, c, f"{v:.6f}"])
 
 
 if __name__ == "__main__":
