@@ -16,12 +16,15 @@
 //      count and symbol workspace; exclusive sums give every payload's first
 //      task and workspace offset; the totals come back to the host (one
 //      small read-back) to size the workspace;
-//   2. scan (bp_scan_kernel): one wave per region; region k > 0 is searched
-//      from its first bit for the first bit offset that passes a cheap filter
+//   2. scan (bp_scan_kernel, two passes, one wave per region): region 0's
+//      candidate is the payload's first bit; region k > 0 is searched for a
+//      stored block (LEN / NLEN, then a look at the block after it), and a
+//      region without one -- in a payload without empty stored blocks (sync
+//      markers) -- for the first bit offset that passes a cheap filter
 //      (block type 2, HLIT <= 29, HDIST <= 29, a complete code-length code by
-//      Kraft sum) and then the full header check above.  Region 0's
-//      candidate is the payload's first bit.  Then (bp_slots_kernel) each
-//      candidate gets a symbol slot sized by its compressed span;
+//      Kraft sum) and then the full header check above.  Then
+//      (bp_slots_kernel) each candidate gets a symbol slot sized by its
+//      compressed span;
 //   3. decode (pmd_inflate_lane3.hip, segment mode): one lane per candidate
 //      from its header to the first block boundary that is the payload's
 //      next candidate, as 16-bit symbols (bp.h); candidates that are not
@@ -379,11 +382,20 @@ bp_region_map_kernel(const uint32_t* __restrict__ nlong, const uint32_t* __restr
 
 // One wave per region (all regions of all long payloads in one index space,
 // so a batch of few payloads still spreads over the chip).
+// Two passes.  Pass 1 (DYN = false) searches every region for a stored
+// block and marks the payload when it finds an empty one (a sync marker, as
+// this library's deflater writes before every chunk of a long message);
+// regions without a stored block are left KIND_PENDING.  Pass 2 (DYN = true)
+// searches the pending regions for dynamic headers -- unless their payload
+// has sync markers, whose chunk starts the stored search already found: a
+// region without one lies inside a chunk, and its bit-offset search would
+// only cost time (a missing candidate just lengthens the segment before it).
+template <bool DYN>
 __global__ void __launch_bounds__(64 * SCAN_WAVES)
 bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                const uint32_t* __restrict__ in_len, const uint32_t* __restrict__ order,
                const uint32_t* __restrict__ region_map, uint32_t n_regions, const Stat* __restrict__ stats,
-               const uint32_t* __restrict__ task_base, SegTask* __restrict__ tasks)
+               const uint32_t* __restrict__ task_base, SegTask* __restrict__ tasks, uint32_t* __restrict__ marked)
 {
     __shared__ ScanLds L;
     for (uint32_t f = threadIdx.x; f < 4096; f += blockDim.x) L.kraft[f] = (uint16_t)kraft4(f);
@@ -397,6 +409,15 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
     const uint32_t waves = gridDim.x * SCAN_WAVES;
     for (uint32_t g = blockIdx.x * SCAN_WAVES + wv; g < n_regions; g += waves) {
         const uint32_t i = (uint32_t)__builtin_amdgcn_readfirstlane((int)region_map[g]);
+        if (DYN) {
+            // only the regions pass 1 left pending, of unmarked payloads
+            const uint32_t kd = (uint32_t)__builtin_amdgcn_readfirstlane((int)tasks[g].kind);
+            if (kd != KIND_PENDING) continue;
+            if (__builtin_amdgcn_readfirstlane((int)marked[i])) {
+                if (lane == 0) tasks[g].kind = KIND_NONE;
+                continue;
+            }
+        }
         const uint32_t m = order[i];
         const Stat st = stats[i];
         const uint32_t len = in_len[m];
@@ -451,12 +472,12 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
                 // 1. stored blocks, by their LEN / NLEN fields (a byte search
                 // over the whole region; this library's deflater writes an
                 // empty one before every chunk of a long message)
-                uint32_t best = 0xffffffffu;
-                for (uint32_t base = b0; base < b1; base += 2048) {
+                uint32_t best = 0xffffffffu, best_len = 0;
+                for (uint32_t base = b0; base < (DYN ? b0 : b1); base += 2048) {
                     const uint32_t first = base + 32 * lane;
                     const uint32_t lb = first + bias;
                     const uint32_t wp = peek32(S, lb - 8), w0 = peek32(S, lb), w1 = peek32(S, lb + 32);
-                    uint32_t found = 0xffffffffu;
+                    uint32_t found = 0xffffffffu, flen = 0;
 #pragma unroll
                     for (uint32_t j = 0; j < 4; ++j) {
                         const uint32_t x = __builtin_amdgcn_alignbit(w1, w0, 8 * j);
@@ -464,12 +485,15 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
                         const uint32_t pb = (first >> 3) + j;
                         const bool c = first + 8 * j < b1 && ((x & 0xffffu) ^ (x >> 16)) == 0xffffu &&
                                        (prevb & 0xc0u) == 0 && pb + 4 + (x & 0xffffu) <= len;
-                        if (c && found == 0xffffffffu && stored_ok(G, Lb, bias, lim, s, len, pb, x & 0xffffu))
+                        if (c && found == 0xffffffffu && stored_ok(G, Lb, bias, lim, s, len, pb, x & 0xffffu)) {
                             found = 8 * pb;
+                            flen = x & 0xffffu;
+                        }
                     }
                     const uint64_t fm = __ballot(found != 0xffffffffu);
                     if (fm) {
                         best = (uint32_t)__builtin_amdgcn_readlane((int)found, (int)__builtin_ctzll(fm));
+                        best_len = (uint32_t)__builtin_amdgcn_readlane((int)flen, (int)__builtin_ctzll(fm));
                         break;
                     }
                 }
@@ -482,7 +506,10 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
                 if (best != 0xffffffffu) {
                     bit = best;
                     kind = KIND_STORED;
+                    if (best_len == 0 && lane == 0) atomicOr(&marked[i], 1u);
                     BP_DIAG(if (lane == 0) atomicAdd(&g_bp_diag[5], 1ull));
+                } else if (!DYN) {
+                    kind = KIND_PENDING;
                 } else {
                     BP_DIAG(if (lane == 0) atomicAdd(&g_bp_diag[6], 1ull));
                     // 2. dynamic headers: block type 2, HLIT / HDIST in range
@@ -888,7 +915,7 @@ extern "C" int bpmd_internal_inflate_bp_run(const uint8_t* in, const uint64_t* i
     unsigned long long* wbase = P.wbase;
     // decode workspace (scratch block 11): tasks, results, fallback list, symbols
     const size_t d_tasks = 0, d_res = al256(d_tasks + sizeof(SegTask) * ntask), d_fb = al256(d_res + sizeof(SegRes) * ntask),
-                 d_map = al256(d_fb + 4ull * n), d_sym = al256(d_map + 4ull * ntask),
+                 d_map = al256(d_fb + 4ull * n), d_mark = al256(d_map + 4ull * ntask), d_sym = al256(d_mark + 4ull * n),
                  dsz = al256(d_sym + 2ull * (nword + SYM_GUARD + 64));
     uint8_t* dw = (uint8_t*)bpmd_internal_scratch(s, dsz, 11);
     if (!dw) return (int)hipErrorOutOfMemory;
@@ -897,12 +924,16 @@ extern "C" int bpmd_internal_inflate_bp_run(const uint8_t* in, const uint64_t* i
     uint32_t* fb = (uint32_t*)(dw + d_fb);
     uint16_t* sym = (uint16_t*)(dw + d_sym);
     uint32_t* rmap = (uint32_t*)(dw + d_map);
+    uint32_t* marked = (uint32_t*)(dw + d_mark);
+    if (hipMemsetAsync(marked, 0, 4ull * n, s) != hipSuccess) return (int)hipErrorUnknown;
     // scan: one wave per region, SCAN_WAVES waves per workgroup, ~3
     // workgroups per CU by LDS; then the slots, one wave per payload
     hipLaunchKernelGGL(bp_region_map_kernel, dim3((n + 255) / 256), dim3(256), 0, s, nlong, reg, tbase, rmap);
     const uint32_t scan_wgs = 3u * cus;
-    hipLaunchKernelGGL(bp_scan_kernel, dim3(scan_wgs), dim3(64 * SCAN_WAVES), 0, s, in, in_off, in_len, order, rmap,
-                       (uint32_t)ntask, st, tbase, tasks);
+    hipLaunchKernelGGL(bp_scan_kernel<false>, dim3(scan_wgs), dim3(64 * SCAN_WAVES), 0, s, in, in_off, in_len, order,
+                       rmap, (uint32_t)ntask, st, tbase, tasks, marked);
+    hipLaunchKernelGGL(bp_scan_kernel<true>, dim3(scan_wgs), dim3(64 * SCAN_WAVES), 0, s, in, in_off, in_len, order,
+                       rmap, (uint32_t)ntask, st, tbase, tasks, marked);
     hipLaunchKernelGGL(bp_slots_kernel, dim3(4u * cus), dim3(256), 0, s, in_len, order, nlong, st, tbase,
                        wbase, tasks);
     if (hipGetLastError() != hipSuccess) return (int)hipErrorUnknown;
