@@ -451,10 +451,13 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
                         const uint32_t j = lane + 64u * u;
                         v[u] = j < nw && q0 + j < E ? A[q0 + j] : 0u;
                     }
+                    // the words past the loaded ones (+ 2 for the peeks at
+                    // the end) read as zeros; the rest of the stage is not
+                    // touched (a 1 KiB region stages ~1.4 KiB, not 8.5)
 #pragma unroll
                     for (uint32_t u = 0; u < U; ++u) {
                         const uint32_t j = lane + 64u * u;
-                        if (j < nwords) S[j] = q0 + j == E - 1 ? v[u] & tailm : v[u];
+                        if (j < nwords && j < nw + 8) S[j] = q0 + j == E - 1 ? v[u] & tailm : v[u];
                     }
                 }
                 if (lane == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
