@@ -143,6 +143,48 @@ LZ_HD uint32_t chain_hash(uint32_t w, unsigned avail, unsigned hbits)
 
 // ---------------------------------------------------------------- Huffman
 //
+// Shannon code lengths for wide alphabets (round 3).  When a block uses at
+// least SHANNON_MIN literal/length symbols (near-random bytes: C5), the
+// optimal Huffman lengths are nearly flat and the serial two-queue merge is
+// the costliest step of the block (~150 K cycles of ~700 K per 4 KiB chunk).
+// There the lengths come from the symbols' own frequencies instead: L(f) =
+// the smallest L >= 1 with f * 2^L >= T (T = the alphabet's total, so the
+// Kraft sum is <= 1), counted per length, the code completed by moving the
+// longest codes up one level while the Kraft sum stays <= 1 (an incomplete
+// literal/length code is an error for inflate_stream, ipp:574-617), and the
+// lengths reassigned in frequency order as gen_bitlen does.  C5 (64 KiB
+// binary): deflate 19.5 -> 23.7 GiB/s at L1, payloads 0.9909 -> 0.9890 of
+// the input (the merge's 15-bit overflow repair costs more here than the
+// Shannon lengths do); never used for narrower alphabets (JSON: 100-150).
+#ifndef BPMD_SHANNON_MIN
+#define BPMD_SHANNON_MIN 200
+#endif
+constexpr unsigned SHANNON_MIN = BPMD_SHANNON_MIN;
+
+LZ_HD unsigned shannon_len(uint32_t f, uint32_t T, unsigned max_bits)
+{
+    unsigned L = (unsigned)(__builtin_clz(f) - __builtin_clz(T));   // f * 2^L in [T / 2, 2T)
+    if (((uint64_t)f << L) < (uint64_t)T) ++L;
+    L = L < 1 ? 1u : L;
+    return L > max_bits ? max_bits : L;
+}
+
+// bl_count[1..max_bits] of a code with Kraft sum <= 1 -> a complete code
+LZ_HD void complete_code(unsigned* bl_count, unsigned max_bits)
+{
+    uint32_t k = 0;
+    for (unsigned b = 1; b <= max_bits; ++b) k += bl_count[b] << (max_bits - b);
+    uint32_t slack = (1u << max_bits) - k;
+    for (unsigned b = max_bits; b >= 2 && slack; --b) {
+        const uint32_t unit = 1u << (max_bits - b);
+        uint32_t n = slack / unit;
+        n = n < bl_count[b] ? n : bl_count[b];
+        bl_count[b] -= n;
+        bl_count[b - 1] += n;
+        slack -= n * unit;
+    }
+}
+//
 // Code lengths for one alphabet.  Deterministic restatement of the
 // two-queue Huffman construction over leaves sorted by (freq, symbol), with
 // the reference's length-limiting rule (deflate_stream.ipp:786-873): leaves
@@ -173,7 +215,9 @@ static inline void sort_u32(uint32_t* a, int n)
 }
 
 // freq[0..n) -> lens[0..n); returns the number of used symbols after dummies.
-static inline int huff_lengths_host(const uint32_t* freq, int n, int max_bits, uint8_t* lens, HuffScratch& S)
+// shannon: the literal/length tree, which takes Shannon lengths when wide.
+static inline int huff_lengths_host(const uint32_t* freq, int n, int max_bits, uint8_t* lens, HuffScratch& S,
+                                    bool shannon = false)
 {
     int m = 0;
     uint32_t f2[N_LCODES + 2];
@@ -187,6 +231,18 @@ static inline int huff_lengths_host(const uint32_t* freq, int n, int max_bits, u
     for (int i = 0; i < n; ++i)
         if (f2[i]) S.key[m++] = (f2[i] << 9) | (uint32_t)i;
     sort_u32(S.key, m);
+    if (shannon && m >= (int)SHANNON_MIN) {
+        uint32_t T = 0;
+        for (int i = 0; i < m; ++i) T += S.key[i] >> 9;
+        unsigned bl[MAX_BITS + 2] = {0};
+        for (int i = 0; i < m; ++i) bl[shannon_len(S.key[i] >> 9, T, (unsigned)max_bits)]++;
+        complete_code(bl, (unsigned)max_bits);
+        int i = m - 1;   // most frequent first gets the shortest
+        for (int bits = 1; bits <= max_bits; ++bits)
+            for (unsigned c = 0; c < bl[bits]; ++c) S.depth[i--] = (uint8_t)bits;
+        for (int j = 0; j < m; ++j) lens[S.key[j] & 511] = S.depth[j];
+        return m;
+    }
     // two-queue merge: leaves 0..m-1, internal nodes m..2m-2
     int li = 0, ii = 0;
     for (int k = 0; k < m - 1; ++k) {

@@ -500,9 +500,11 @@ __device__ void build_trees(HuffLds& H, Prof& pf)
     }
     pf.lap(4);
     const unsigned ml = used_l, md = used_d;
+    // a wide literal/length alphabet takes Shannon lengths (lz_core.h), no merge
+    const bool shan = ml >= lz::SHANNON_MIN;
     // --- merges (lane 0: lit, lane 1: dist)
     if (lane < 2) {
-        if (lane == 0) merge_tree(H, 0, ml, 0, 0);
+        if (lane == 0) { if (!shan) merge_tree(H, 0, ml, 0, 0); }
         else merge_tree(H, ml, md, 288, 576);
     }
     wave_sync();
@@ -516,7 +518,7 @@ __device__ void build_trees(HuffLds& H, Prof& pf)
             const unsigned v = lane + t * WAVE;
             const bool lit = v < 576;
             const unsigned root = lit ? root_l : root_d;
-            const bool valid = lit ? v <= root_l : (v >= 576 && v <= root_d);
+            const bool valid = lit ? (!shan && v <= root_l) : (v >= 576 && v <= root_d);
             anc[t] = valid && v != root ? (unsigned)H.parent[v] + (lit ? 0u : 576u) : v;
             dep[t] = valid && v != root ? 1u : 0u;
             if (valid) {
@@ -543,7 +545,7 @@ __device__ void build_trees(HuffLds& H, Prof& pf)
             for (unsigned t = 0; t < NODES_PER_LANE; ++t) {
                 const unsigned v = lane + t * WAVE;
                 const bool lit = v < 576;
-                const bool valid = lit ? v <= root_l : (v >= 576 && v <= root_d);
+                const bool valid = lit ? (!shan && v <= root_l) : (v >= 576 && v <= root_d);
                 if (valid) {
                     H.parent[v] = (uint16_t)anc[t];
                     H.depth[v] = (uint8_t)dep[t];
@@ -557,19 +559,25 @@ __device__ void build_trees(HuffLds& H, Prof& pf)
     // --- length limit (15) and per-length counts
     for (unsigned i = lane; i < 32; i += WAVE) H.blcount[i >> 4][i & 15] = 0;
     wave_sync();
+    uint32_t T = 0;   // Shannon lengths: the literal/length alphabet's total
+    if (shan) {
+        for (unsigned i = lane; i < ml; i += WAVE) T += H.keys[i] >> 9;
+        T = wave_sum(T);
+    }
     unsigned ovf_l = 0, ovf_d = 0;
     for (unsigned i = lane; i < ml + md; i += WAVE) {
         const bool lit = i < ml;
         const unsigned v = lit ? i : 576 + (i - ml);
-        unsigned d = H.depth[v];
+        unsigned d = lit && shan ? lz::shannon_len(H.keys[i] >> 9, T, lz::MAX_BITS) : H.depth[v];
         if (d > lz::MAX_BITS) { d = lz::MAX_BITS; if (lit) ++ovf_l; else ++ovf_d; }
         atomicAdd(&H.blcount[lit ? 0 : 1][d], 1u);
     }
     ovf_l = wave_sum(ovf_l);
     ovf_d = wave_sum(ovf_d);
     wave_sync();
-    if (ovf_l | ovf_d) {
-        if (lane < 2) {
+    if (ovf_l | ovf_d | (shan ? 1u : 0u)) {
+        if (lane == 0 && shan) lz::complete_code(H.blcount[0], lz::MAX_BITS);
+        if (lane < 2 && !(lane == 0 && shan)) {
             int overflow = (int)(lane == 0 ? ovf_l : ovf_d);
             uint32_t* bc = H.blcount[lane];
             while (overflow > 0) {
@@ -585,7 +593,7 @@ __device__ void build_trees(HuffLds& H, Prof& pf)
         // reassign: the r-th most frequent leaf gets the r-th shortest length
         for (unsigned i = lane; i < ml + md; i += WAVE) {
             const bool lit = i < ml;
-            if ((lit ? ovf_l : ovf_d) == 0) continue;
+            if ((lit ? (ovf_l || shan) : ovf_d) == 0) continue;
             const unsigned m = lit ? ml : md, leaf = lit ? i : i - ml;
             const unsigned r = m - 1 - leaf;
             const uint32_t* bc = H.blcount[lit ? 0 : 1];

@@ -206,7 +206,7 @@ static std::vector<uint8_t> encode(const uint8_t* msg, unsigned n, const Params&
         lf[EOB] = 1;
         Coder dyn, fix;
         HuffScratch S;
-        huff_lengths_host(lf, N_LCODES, MAX_BITS, dyn.llen, S);
+        huff_lengths_host(lf, N_LCODES, MAX_BITS, dyn.llen, S, true);
         huff_lengths_host(df, N_DCODES, MAX_BITS, dyn.dlen, S);
         int lcodes = N_LCODES, dcodes = N_DCODES;
         while (lcodes > 257 && dyn.llen[lcodes - 1] == 0) --lcodes;
