@@ -152,6 +152,9 @@ __global__ void bp_totals_kernel(const uint32_t* __restrict__ regions, const uin
 #define BP_DIAG(x)
 #endif
 __device__ unsigned long long g_bp_diag[12];
+// the last payload that fell back to the wave kernel (bpmd_diag_bp_fallback):
+// message, segment (task - first task), segment status, symbols, slot symbols
+__device__ uint32_t g_bp_fb[8];
 
 // ------------------------------------------------------------------ scan
 __device__ __forceinline__ uint32_t wave_lane() { return threadIdx.x & 63u; }
@@ -784,6 +787,16 @@ bp_resolve_kernel(const uint32_t* __restrict__ order, const uint32_t* __restrict
             }
             if (r.status == SEG_FULL || r.status == SEG_SKIP || r.status == SEG_HANDOFF) {
                 fallback = true;
+                if (lane == 0) {
+                    g_bp_fb[0] = m;
+                    g_bp_fb[1] = t - task_base[i];
+                    g_bp_fb[2] = (uint32_t)r.status;
+                    g_bp_fb[3] = r.nsym;
+                    g_bp_fb[4] = tasks[t].sym_cap;
+                    g_bp_fb[5] = r.next;
+                    g_bp_fb[6] = tasks[t].bit;
+                    g_bp_fb[7] = tasks[t].kind;
+                }
                 break;
             }
             stv = r.status;
@@ -963,6 +976,11 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
     if (e || ntask == 0) return e;
     return bpmd_internal_inflate_bp_run(in, in_off, in_len, out, out_off, out_cap, out_len, status, raw, order, nlong,
                                         s);
+}
+
+extern "C" int bpmd_diag_bp_fallback(uint32_t* out8)
+{
+    return hipMemcpyFromSymbol(out8, HIP_SYMBOL(bpmd::bp::g_bp_fb), sizeof(uint32_t) * 8) == hipSuccess ? 0 : -1;
 }
 
 // diagnostics: the 12 counters of g_bp_diag (out[12]); reset after reading
