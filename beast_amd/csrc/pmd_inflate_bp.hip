@@ -116,9 +116,10 @@ bp_stats_kernel(const uint32_t* __restrict__ in_len, const uint32_t* __restrict_
         s.regions = na;
         s.R = (uint32_t)R;
         s.F16 = (uint32_t)((e16 * 5) >> 2);
-        // slots: span (rounded up to bytes, so at most len + na) x F16, plus
-        // SLACK each, after the payload's guard
-        w = ((((unsigned long long)len + na) * s.F16) >> 16) + (unsigned long long)SLACK * na + SYM_GUARD + 64;
+        // slots: span to the candidate after next (rounded up to bytes; the
+        // spans add up to at most 2 (len + na)) x F16, plus SLACK each, after
+        // the payload's guard
+        w = ((((unsigned long long)2 * (len + na)) * s.F16) >> 16) + (unsigned long long)SLACK * na + SYM_GUARD + 64;
     }
     st[i] = s;
     regions[i] = na;
@@ -620,31 +621,44 @@ bp_slots_kernel(const uint32_t* __restrict__ in_len, const uint32_t* __restrict_
         const uint32_t len = in_len[order[i]];
         const uint32_t tb = task_base[i];
         uint64_t run = word_base[i] + SYM_GUARD;
-        uint32_t nextbit = 8 * len;   // the next candidate's bit, from the chunk after
+        // A slot reaches to the candidate after next: a false candidate (a
+        // random LEN / NLEN whose LEN happens to land on a real block start,
+        // ~1 per GiB of binary payload) that precedes a region's real one
+        // must not size the real segment's slot to its own short span.
+        uint32_t n1 = 8 * len, n2 = 8 * len;   // the two next candidates' bits, from the chunks after
         const uint32_t nch = (st.regions + 63) / 64;
-        // chunks from the last to the first (suffix "next candidate" scan),
-        // slot offsets assigned afterwards from the first
+        auto two_min = [](uint32_t& a1, uint32_t& a2, uint32_t b1, uint32_t b2) {
+            const uint32_t lo = a1 < b1 ? a1 : b1, hi = a1 < b1 ? b1 : a1;
+            const uint32_t m = a2 < b2 ? a2 : b2;
+            a1 = lo;
+            a2 = hi < m ? hi : m;
+        };
+        // chunks from the last to the first (suffix scans of the two smallest
+        // candidate bits), slot offsets assigned afterwards from the first
         SegTask* vt = tasks + tb;
         for (uint32_t c = nch; c-- > 0;) {
             const uint32_t k = c * 64 + lane;
             const bool v = k < st.regions && vt[k].kind != KIND_NONE;
             const uint32_t b = v ? vt[k].bit : 0xffffffffu;
-            // the next candidate's bit after k: the inclusive suffix min of
-            // the chunk, one lane up (then the chunk after's first)
-            uint32_t sm = b;
+            uint32_t s1 = b, s2 = 0xffffffffu;   // inclusive suffix: the two smallest from k on
             for (uint32_t d = 1; d < 64; d <<= 1) {
-                const uint32_t y = __shfl_down(sm, d);
-                sm = lane + d < 64 && y < sm ? y : sm;
+                const uint32_t y1 = __shfl_down(s1, d), y2 = __shfl_down(s2, d);
+                if (lane + d < 64) two_min(s1, s2, y1, y2);
             }
-            uint32_t after = __shfl_down(sm, 1);
-            after = lane == 63 ? 0xffffffffu : after;
-            after = after == 0xffffffffu ? nextbit : after;
+            // the two candidates after k: lane k + 1's suffix, then the chunks after
+            uint32_t a1 = __shfl_down(s1, 1), a2 = __shfl_down(s2, 1);
+            if (lane == 63) a1 = a2 = 0xffffffffu;
+            two_min(a1, a2, n1, n2);
             if (v) {
+                const uint32_t after = a2 < 8 * len ? a2 : 8 * len;
                 const uint32_t span = after > b ? (after - b + 7) >> 3 : 1u;
                 vt[k].sym_cap = (uint32_t)(((uint64_t)span * st.F16) >> 16) + SLACK;
             }
-            const uint32_t first_b = __shfl(sm, 0);
-            nextbit = first_b == 0xffffffffu ? nextbit : first_b;
+            const uint32_t f1 = __shfl(s1, 0), f2 = __shfl(s2, 0);
+            uint32_t c1 = f1, c2 = f2;
+            two_min(c1, c2, n1, n2);
+            n1 = c1;
+            n2 = c2;
         }
         __builtin_amdgcn_s_waitcnt(0);
         __builtin_amdgcn_wave_barrier();
