@@ -27,14 +27,7 @@ extern "C" int bpmd_internal_inflate_lane3(const uint8_t* in, const uint64_t* in
                                            uint32_t* out_len, int32_t* status, uint32_t raw, const uint32_t* mask_key,
                                            const uint32_t* hist_len, uint32_t hist_max, uint32_t max_in,
                                            const uint32_t* order, uint32_t* qctr, uint32_t grid_wgs,
-                                           const uint32_t* skip, hipStream_t stream, const uint32_t* n_dev);
-extern "C" int bpmd_internal_inflate_lane4(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n,
-                                           uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
-                                           uint32_t* out_len, int32_t* status, uint32_t raw, const uint32_t* mask_key,
-                                           const uint32_t* hist_len, uint32_t hist_max, uint32_t max_in,
-                                           const uint32_t* order, uint32_t* qctr, uint32_t grid_wgs,
                                            const uint32_t* skip, hipStream_t stream);
-extern "C" uint32_t bpmd_internal_lane4_per_cu(void);
 extern "C" const uint32_t* bpmd_internal_lane_order(const uint32_t* in_len, uint32_t n, hipStream_t stream,
                                                     const uint32_t** keys_out);
 extern "C" const uint32_t* bpmd_internal_lane_long_split(const uint32_t* in_len, const uint32_t* keys, uint32_t n,
@@ -192,8 +185,7 @@ uint8_t* scratch_for(hipStream_t s, size_t bytes, int which = 0)
 // scratch block `which` (0 inflate queue, 1-2 deflate workspace, 3-4 exact
 // deflate queue and workspace, 5 inflate message order, 6 wave inflate queue,
 // 7 deflate chunk queue, 8 multi-device output totals, 9 long-payload split,
-// 10-11 block-parallel inflate stats and decode workspace, 12-13 lane4
-// hand-back list and its queue)
+// 10-11 block-parallel inflate stats and decode workspace)
 // for other translation units
 extern "C" void* bpmd_internal_scratch(hipStream_t s, size_t bytes, int which)
 {
@@ -252,20 +244,18 @@ extern "C" const char* bpmd_version(void) { return "beast_pmd 0.2 (gfx950)"; }
 extern "C" unsigned bpmd_diag_grid_override = 0;
 extern "C" void bpmd_diag_set_grid(unsigned grid) { bpmd_diag_grid_override = grid; }
 
-// Kernel choice for a batch: one lane per message (pmd_inflate_lane4.hip,
-// table-driven; the canonical-search lane3 kernel decodes what it hands back)
+// Kernel choice for a batch: one lane per message (pmd_inflate_lane3.hip)
 // for throughput, one wave per message (pmd_inflate.hip) for latency when
 // the batch is too small to fill the chip's lanes, and block-parallel decode
 // (pmd_inflate_bp.hip) for the long payloads of large batches.
-// BPMD_INFLATE=lane|wave|bp|lane3 or bpmd_set_inflate_kernel() forces one
-// (the tests run all of them; "bp" sends every payload of 64 bytes or more
-// through the block-parallel path; "lane3" is the lane mode on the lane3
-// kernel alone).
-static std::atomic<int> g_inflate_kernel{-1};   // -1 unset, 0 auto, 1 lane, 2 wave, 3 bp, 4 lane3
+// BPMD_INFLATE=lane|wave|bp or bpmd_set_inflate_kernel() forces one (the
+// tests run all three; "bp" sends every payload of 64 bytes or more through
+// the block-parallel path).
+static std::atomic<int> g_inflate_kernel{-1};   // -1 unset, 0 auto, 1 lane, 2 wave, 3 bp
 
 extern "C" int bpmd_set_inflate_kernel(int mode)
 {
-    if (mode < 0 || mode > 4) return BPMD_R_INVALID_ARGUMENT;
+    if (mode < 0 || mode > 3) return BPMD_R_INVALID_ARGUMENT;
     g_inflate_kernel.store(mode);
     return BPMD_R_OK;
 }
@@ -275,8 +265,7 @@ static int inflate_mode()
     int m = g_inflate_kernel.load();
     if (m < 0) {
         const char* e = getenv("BPMD_INFLATE");
-        m = (e && !strcmp(e, "lane")) ? 1 : (e && !strcmp(e, "wave")) ? 2 : (e && !strcmp(e, "bp")) ? 3
-            : (e && !strcmp(e, "lane3")) ? 4 : 0;
+        m = (e && !strcmp(e, "lane")) ? 1 : (e && !strcmp(e, "wave")) ? 2 : (e && !strcmp(e, "bp")) ? 3 : 0;
         g_inflate_kernel.store(m);
     }
     return m;
@@ -345,22 +334,6 @@ int inflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
     if (!mu) return BPMD_R_HIP_ERROR;
     std::lock_guard<std::mutex> launch(*mu);
     const int m = inflate_mode();
-    // the lane kernel: lane4 (mode 4: lane3 alone), and the lanes it keeps resident
-    const bool v3 = m == 4;
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const uint32_t per_cu = v3 ? 256u : bpmd_internal_lane4_per_cu();   // messages in flight per CU
-    const uint32_t wg_lanes = v3 ? 64u : 32u;
-    auto lane_run = [&](uint32_t max_in, const uint32_t* order, uint32_t* qctr, uint32_t grid_wgs,
-                        const uint32_t* skip) -> int {
-        if (v3)
-            return bpmd_internal_inflate_lane3(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
-                                               d_status, raw, key, hist, 1u << cfg->window_bits, max_in, order, qctr,
-                                               grid_wgs, skip, s, nullptr);
-        return bpmd_internal_inflate_lane4(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
-                                           d_status, raw, key, hist, 1u << cfg->window_bits, max_in, order, qctr,
-                                           grid_wgs, skip, s);
-    };
     // block-parallel decode applies to plain batches (no takeover window, no
     // masking key: the segment decoder starts mid-payload)
     const bool bp_ok = !hist && !key && ((m == 0 && inflate_bp_enabled()) || m == 3);
@@ -371,13 +344,15 @@ int inflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
         const uint32_t* nlong = order ? bpmd_internal_lane_long_split(d_in_len, keys, n_msgs, 0u, 64u, 0u, s) : nullptr;
         if (!nlong || bpmd_internal_inflate_bp(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap,
                                                d_out_len, d_status, raw, order, nlong, s) ||
-            lane_run(0u, order, nullptr, 0u, nlong))
+            bpmd_internal_inflate_lane3(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
+                                        d_status, raw, nullptr, nullptr, 1u << cfg->window_bits, 0u, order, nullptr,
+                                        0u, nlong, s))
             return BPMD_R_HIP_ERROR;
         return BPMD_R_OK;
     }
     // lane-kernel share: everything (hist / forced lane), nothing (forced wave /
     // small batch), or the payloads of at most `split` bytes
-    const bool lane = hist || m == 1 || m == 4 || (m == 0 && n_msgs >= 2048);
+    const bool lane = hist || m == 1 || (m == 0 && n_msgs >= 2048);
     // from 32 Ki messages on, the lanes fill the chip whatever the sizes: no
     // split, and no second launch (C2 +1.6 %, C4 lane-only 23.2 vs 22.6 GiB/s)
     const uint32_t split = (hist || m != 0 || n_msgs >= 32768) ? 0u : inflate_split();
@@ -385,7 +360,9 @@ int inflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
     if (lane) {
         // more messages than the chip holds lanes: a work queue keeps every
         // lane busy until the batch is done (mixed sizes, configs[3])
-        uint32_t wgs = per_cu / wg_lanes * (uint32_t)cus;   // resident workgroups
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        uint32_t wgs = 4u * (uint32_t)cus;   // 4 workgroups of 64 messages per CU are resident
         // diagnostics / tests: BPMD_QUEUE_WGS caps the grid so that small batches
         // run through the work queue too
         static const uint32_t q_override = [] {
@@ -396,7 +373,7 @@ int inflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
         uint32_t* qctr = nullptr;
         const uint32_t* order = nullptr;
         const uint32_t* nlong = nullptr;
-        if (n_msgs > wgs * wg_lanes && !split) {
+        if (n_msgs > wgs * 64u && !split) {
             qctr = (uint32_t*)scratch_for(s, 256);
             if (!qctr || hipMemsetAsync(qctr, 0, sizeof(uint32_t), s) != hipSuccess) return BPMD_R_HIP_ERROR;
             // longest first, so no lane starts a long message as the batch drains
@@ -421,8 +398,8 @@ int inflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
                     const char* e = getenv("BPMD_LONG_SHARE_PCT");
                     return e ? (uint32_t)strtoul(e, nullptr, 10) : 50u;
                 }();
-                if (!(nlong = bp_ok ? bpmd_internal_lane_long_split(d_in_len, keys, n_msgs, wgs * wg_lanes, 2048u, share_pct, s)
-                                    : bpmd_internal_lane_long_split(d_in_len, keys, n_msgs, wgs * wg_lanes, 4096u, 200u, s)))
+                if (!(nlong = bp_ok ? bpmd_internal_lane_long_split(d_in_len, keys, n_msgs, wgs * 64u, 2048u, share_pct, s)
+                                    : bpmd_internal_lane_long_split(d_in_len, keys, n_msgs, wgs * 64u, 4096u, 200u, s)))
                     return BPMD_R_HIP_ERROR;
                 if (bp_ok) {
                     // the lane kernel on the caller's stream (it skips the long
@@ -437,7 +414,9 @@ int inflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
                     // (behind the lane kernel it would wait for a free CU)
                     uint64_t ntask = 0;
                     int eb = bpmd_internal_inflate_bp_plan(d_in_len, n_msgs, d_out_cap, order, nlong, sd.side, &ntask);
-                    e = lane_run(0u, order, qctr, wgs, nlong);
+                    e = bpmd_internal_inflate_lane3(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap,
+                                                    d_out_len, d_status, raw, key, hist, 1u << cfg->window_bits, 0u,
+                                                    order, qctr, wgs, nlong, s);
                     if (!eb && ntask)
                         eb = bpmd_internal_inflate_bp_run(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_cap,
                                                           d_out_len, d_status, raw, order, nlong, sd.side);
@@ -458,10 +437,14 @@ int inflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
                 bpmd_internal_inflate_bp(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
                                          d_status, raw, order, nlong, s))
                 return BPMD_R_HIP_ERROR;
-            e = lane_run(0u, order, nullptr, wgs, nlong);
+            e = bpmd_internal_inflate_lane3(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
+                                            d_status, raw, key, hist, 1u << cfg->window_bits, 0u, order, nullptr, wgs,
+                                            nlong, s);
             return e ? BPMD_R_HIP_ERROR : BPMD_R_OK;
         }
-        e = lane_run(split, order, qctr, wgs, nlong);
+        e = bpmd_internal_inflate_lane3(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
+                                        d_status, raw, key, hist, 1u << cfg->window_bits, split, order, qctr, wgs,
+                                        nlong, s);
     }
     if (!e && (!lane || split))
         e = bpmd_internal_inflate_keyed_split(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap,

@@ -1019,7 +1019,9 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
             if (SEG) {
                 // the next candidate is this stored block (its LEN field)
                 cur = vbase + (uint32_t)((int32_t)vtot - avail);
-                if (nk_bit == cur && nk_kind == bp::KIND_STORED) {
+                // (not for a final stored block: the candidate's segment would
+                // start without its BFINAL bit and miss the end of the stream)
+                if (nk_bit == cur && nk_kind == bp::KIND_STORED && !last) {
                     result = bp::SEG_HANDOFF;
                     st = S_DONE;
                 }
@@ -1392,7 +1394,7 @@ inflate_lane3_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict_
                      uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t raw,
                      const uint32_t* __restrict__ mask_key, const uint32_t* __restrict__ hist_len, uint32_t hist_max,
                      uint32_t max_in, const uint32_t* __restrict__ order, uint32_t* __restrict__ qctr,
-                     const uint32_t* __restrict__ skip, const uint32_t* __restrict__ n_dev)
+                     const uint32_t* __restrict__ skip)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const unsigned lane = threadIdx.x & 63u;
@@ -1401,8 +1403,6 @@ inflate_lane3_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict_
     // skip: the first *skip entries of `order` belong to the wave kernel (the
     // long payloads of a work-queue batch, pmd_capi.hip inflate_impl)
     const uint32_t s0 = skip ? *skip : 0u;
-    // n_dev: a device-side count (the lane4 kernel's hand-back list)
-    if (n_dev && *n_dev < n_msgs) n_msgs = *n_dev;
     // first message: slot s0 + blockIdx.x * 64 + lane (of `order` when given)
     const uint32_t j = s0 + blockIdx.x * WG_MSGS + lane;
     bool valid = j < n_msgs;
@@ -1470,7 +1470,7 @@ extern "C" int bpmd_internal_inflate_lane3(const uint8_t* in, const uint64_t* in
                                            uint32_t* out_len, int32_t* status, uint32_t raw, const uint32_t* mask_key,
                                            const uint32_t* hist_len, uint32_t hist_max, uint32_t max_in,
                                            const uint32_t* order, uint32_t* qctr, uint32_t grid_wgs,
-                                           const uint32_t* skip, hipStream_t stream, const uint32_t* n_dev)
+                                           const uint32_t* skip, hipStream_t stream)
 {
     using namespace bpmd::lp3;
     if (n == 0) return 0;
@@ -1478,7 +1478,7 @@ extern "C" int bpmd_internal_inflate_lane3(const uint8_t* in, const uint64_t* in
     if (qctr && grid_wgs && grid > grid_wgs) grid = grid_wgs;
     hipLaunchKernelGGL(inflate_lane3_kernel, dim3(grid), dim3(128), WG_MSGS * STRIDE, stream, in, in_off, in_len, n,
                        out, out_off, out_cap, out_len, status, raw, mask_key, hist_len, hist_max, max_in, order, qctr,
-                       skip, n_dev);
+                       skip);
     return (int)hipGetLastError();
 }
 
@@ -1564,11 +1564,13 @@ __global__ void long_count_kernel(const uint32_t* __restrict__ keys, uint32_t n,
     const unsigned long long total = split[0];
     unsigned long long thr = lanes ? (unsigned long long)share_pct * total / (100ull * lanes) : 0ull;
     if (thr < min_thr) thr = min_thr;
-    const uint32_t tk = (uint32_t)((thr + 63) >> 6);   // long: key > tk (keys descending)
+    // long: key >= ceil(thr / 64), i.e. in_len >= thr when thr is a multiple
+    // of 64 (every caller's), at least thr otherwise (keys descending)
+    const uint32_t tk = (uint32_t)((thr + 63) >> 6);
     uint32_t lo = 0, hi = n;
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
-        if (keys[mid] > tk) lo = mid + 1;
+        if (keys[mid] >= tk) lo = mid + 1;
         else hi = mid;
     }
     ((uint32_t*)split)[2] = lo;

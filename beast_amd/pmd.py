@@ -62,7 +62,6 @@ def lib():
         L.bpmd_inflate_batch.restype = ctypes.c_int
         L.bpmd_deflate_batch.argtypes = [ctypes.POINTER(_Cfg), vp, vp, vp, ctypes.c_uint32, vp, vp, vp, vp, vp, vp]
         L.bpmd_diag_set_wave_walk.argtypes = [ctypes.c_int]
-        L.bpmd_diag_set_lane4_sub.argtypes = [ctypes.c_int, ctypes.c_int]
         L.bpmd_diag_bp_counters.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
         L.bpmd_shard_ranges.argtypes = [vp, ctypes.c_uint32, ctypes.c_int, vp]
         L.bpmd_inflate_batch_multi.argtypes = [ctypes.POINTER(_Cfg), vp, ctypes.c_int, vp]

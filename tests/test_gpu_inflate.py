@@ -14,28 +14,21 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 
-@pytest.fixture(autouse=True, params=["lane", "lane_handback", "lane3", "wave", "wave_walk", "wave_spec", "bp"])
+@pytest.fixture(autouse=True, params=["lane", "wave", "wave_walk", "wave_spec", "bp"])
 def inflate_kernel(request):
-    """Every inflate test runs on every kernel, forced through
-    bpmd_set_inflate_kernel: the table-driven lane kernel
-    (pmd_inflate_lane4.hip), the same with zero sub-table budgets so that
-    every block with a code longer than its root bits is handed back to the
-    lane3 kernel (bpmd_diag_set_lane4_sub), the canonical-search lane kernel
-    alone (pmd_inflate_lane3.hip), the wave kernel (pmd_inflate.hip), also
-    with every round a walk round and with speculative rounds only
-    (bpmd_diag_set_wave_walk), and block-parallel (pmd_inflate_bp.hip: every
+    """Every inflate test runs on both kernels (pmd_inflate_lane3.hip and
+    pmd_inflate.hip), forced through bpmd_set_inflate_kernel; the wave kernel
+    also with every round a walk round and with speculative rounds only
+    (bpmd_diag_set_wave_walk); and block-parallel (pmd_inflate_bp.hip: every
     payload of 64 bytes or more cut at its dynamic-block headers)."""
     pmd = _pmd()
-    mode = {"lane": 1, "lane_handback": 1, "lane3": 4, "wave": 2, "wave_walk": 2, "wave_spec": 2,
-            "bp": 3}[request.param]
+    mode = {"lane": 1, "wave": 2, "wave_walk": 2, "wave_spec": 2, "bp": 3}[request.param]
     walk = {"wave_walk": 1, "wave_spec": 2}.get(request.param, 0)
     assert pmd.lib().bpmd_set_inflate_kernel(mode) == 0
     assert pmd.lib().bpmd_diag_set_wave_walk(walk) == 0
-    assert pmd.lib().bpmd_diag_set_lane4_sub(*((0, 0) if request.param == "lane_handback" else (-1, -1))) == 0
     yield request.param
     pmd.lib().bpmd_set_inflate_kernel(0)
     pmd.lib().bpmd_diag_set_wave_walk(0)
-    pmd.lib().bpmd_diag_set_lane4_sub(-1, -1)
 
 
 def _pmd():

@@ -167,3 +167,21 @@ def test_auto_mixed_batch_takes_bp():
         payloads.append(O.pmd_deflate(data, rng.choice([1, 6]), 15, 4))
         caps.append(size)
     _check(payloads, caps)
+
+
+@pytest.mark.parametrize("raw", [False, True])
+def test_final_stored_block_keeps_end_of_stream(mode, raw):
+    """zlib's Z_FINISH on incompressible data ends with a final (BFINAL=1)
+    stored block, which the scan can also find as a stored candidate; the
+    segment that reaches it must keep its BFINAL bit, so the message ends
+    with end_of_stream (raw) or fails the pmd tail, as the serial decoder
+    does (RFC 7692 allows a sender to finish a message that way)."""
+    rng = random.Random(0xF1)
+    payloads, caps = [], []
+    for _ in range(12):
+        size = rng.randrange(9000, 150000)
+        data = rng.randbytes(size)
+        c = zlib.compressobj(rng.choice([1, 6]), zlib.DEFLATED, -15)
+        payloads.append(c.compress(data) + c.flush(zlib.Z_FINISH))
+        caps.append(size + 16)
+    _check(payloads, caps, raw=raw)
