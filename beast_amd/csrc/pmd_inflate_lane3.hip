@@ -77,6 +77,10 @@ constexpr uint32_t TOK_STORED = 0x10000000u;  // segment mode: bits 0-15 stored 
 #ifndef BPMD3_ESLEEP
 #define BPMD3_ESLEEP 8
 #endif
+#ifndef BPMD3_KX
+#define BPMD3_KX 4
+#endif
+constexpr int KX = BPMD3_KX;   // expander pieces per iteration
 #ifndef BPMD3_DPRIO
 #define BPMD3_DPRIO 3
 #endif
@@ -121,6 +125,14 @@ __device__ unsigned long long g_l3prof[16];
 static __constant__ const uint8_t kClenOrder2[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
 // ------------------------------------------------------------------ expander
+// Up to KX pieces per iteration -- a token's literal bytes and one chunk of
+// its match -- are taken from the ring, and every match chunk whose source
+// lies wholly below the output already stored (F) is loaded in the same
+// iteration, so the pieces' loads are in flight together; they are stored at
+// the start of the next iteration, in output order (a store's spare bytes
+// past its piece are overwritten by the next store).  A match whose source
+// reaches into pieces not yet stored ends the batch.  Distances below 8
+// become a pattern register built from the 8 bytes before the match.
 __device__ __forceinline__ void expander(uint8_t* T, bool valid, uint32_t m, uint8_t* __restrict__ out,
                                          const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
                                          uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
@@ -134,161 +146,180 @@ __device__ __forceinline__ void expander(uint8_t* T, bool valid, uint32_t m, uin
         hist = hist_len ? (hist_len[mm] < hist_max ? hist_len[mm] : hist_max) : 0u;
     };
     if (valid) slot(m);
-    bool done = !valid;            // the lane's message is complete (END taken)
-    bool exited = !queue && done;  // no token will come any more
-    uint32_t tail = 0, pos = 0;
-    // match copy: bytes left to issue, distance, next output position
+    bool exited = !queue && !valid;   // no token will come any more
+    uint32_t tail = 0, pos = 0;       // pos: output position after every piece taken
+    // the match being copied: bytes left, distance, next output position
     uint32_t crem = 0, cdist = 0, cq = 0;
     uint64_t cpat = 0;
-    uint32_t cpat_st = 0;   // dist < 8: 0 pattern not requested, 1 source bytes in flight, 2 pattern ready
-    // chunk loaded in the previous memory section, stored in the next one
-    bool cst = false, cst_pat = false;
-    uint32_t cdst = 0, csz = 0, cpd = 1, csh = 0;
-    uint4 cw = make_uint4(0, 0, 0, 0), cw2 = cw;
-    // literal bytes of the previous token, stored in the next memory section
-    uint32_t bcnt = 0, bdst = 0, bval = 0;
+    uint32_t cpat_st = 0;   // dist < 8: 0 pattern not requested, 1 requested, 2 ready
+    // pieces taken in the previous iteration, stored at the start of this one
+    uint32_t l_dst[KX], l_val[KX], l_n[KX], m_dst[KX], m_sz[KX], m_pat[KX];
+    uint4 m_w[KX];
+#pragma unroll
+    for (int j = 0; j < KX; ++j) {
+        l_dst[j] = l_val[j] = l_n[j] = m_dst[j] = m_sz[j] = m_pat[j] = 0;
+        m_w[j] = make_uint4(0, 0, 0, 0);
+    }
     L3_DECL;
     for (;;) {
-        const bool alive = !exited || crem != 0 || cst || bcnt != 0;
-        if (!__ballot(alive)) break;
-        L3_CNT(1);
-        bool worked = cst || bcnt != 0 || crem != 0;
-        // ================================================ memory section
-        // Stores go in output order (a chunk's spare tail bytes are always
-        // overwritten by a later store), and every load of earlier output is
-        // issued after the stores it reads; each loaded chunk is stored one
-        // iteration later.
-        if (cst) {
-            uint4 w = cw;
-            if (cst_pat) {
-                // the cpd bytes before the match, repeated with period cpd (the
-                // match that asked for them may be finished and a new one
-                // started since: its distance is the request's own, cpd)
-                uint64_t v = ((uint64_t)cw.y << 32) | cw.x;
-                v >>= 8 * csh;
-                v &= (1ull << (8 * cpd)) - 1;
-                // (64-bit shifts of 64 or more wrap on the hardware: guard them)
-                if (cpd < 8) v |= v << (8 * cpd);
-                if (cpd < 4) v |= v << (16 * cpd);
-                if (cpd < 2) v |= v << (32 * cpd);
-                if (cpat_st == 1) {   // still the current match
-                    cpat = v;
-                    cpat_st = 2;
-                }
-                w = make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0, 0);
-            }
-            if (csz == 32) {
-                // the chunk's used bytes pass cdst + 16, so both halves start inside the slot
-                store_bounded(o, cdst, 16, cap, w);
-                store_bounded(o, cdst + 16, 16, cap, cw2);
-            } else {
-                store_bounded(o, cdst, csz, cap, w);
-            }
-            cst = false;
-            cst_pat = false;
-        }
-        if (bcnt) {
-            // one dword store (bytes past bcnt are overwritten by later
-            // output, as a chunk's spare tail), bytes only at the slot's end
-            if (bdst + 4 <= cap) {
-                *(uint32_u*)(o + bdst) = bval;
-            } else {
+        bool pending = false;
 #pragma unroll
-                for (uint32_t j = 0; j < 4; ++j)
-                    if (j < bcnt) o[bdst + j] = (uint8_t)(bval >> (8 * j));
-            }
-            bcnt = 0;
-        }
-        if (crem) {
-            // 32 bytes per iteration when the source lies a whole 32 back
-            const uint32_t C = (cdist >= 32 && crem > 16) ? 32u : cdist >= 16 ? 16u : 8u;
-            bool ld = false;
-            int32_t src = 0;   // < 0: in the window before the slot
-            if (cdist < 8) {
-                const uint32_t adv0 = 8 - 8 % cdist;
-                const uint32_t adv = adv0 < crem ? adv0 : crem;
-                if (cpat_st == 2) {
-                    const uint4 pw = make_uint4((uint32_t)cpat, (uint32_t)(cpat >> 32), 0, 0);
-                    store_bounded(o, cq, 8, cap, pw);
-                    cq += adv;
-                    crem -= adv;
-                } else if (cpat_st == 0) {
-                    // the cdist bytes before cq, read as 8 bytes that never
-                    // start before the slot's window
-                    ld = true;
-                    src = max((int32_t)cq - 8, -(int32_t)hist);
-                    csh = (uint32_t)((int32_t)cq - (int32_t)cdist - src);
-                    cst_pat = true;
-                    cpd = cdist;
-                    csz = 8;
-                    cpat_st = 1;
-                    cdst = cq;
-                    cq += adv;
-                    crem -= adv;
+        for (int j = 0; j < KX; ++j) pending = pending || l_n[j] != 0 || m_sz[j] != 0;
+        if (!__ballot(!exited || crem != 0 || pending)) break;
+        L3_CNT(1);
+        bool worked = pending;
+        // ================================================ stores, output order
+        // (a store's bytes past its piece are overwritten by the next one)
+#pragma unroll
+        for (int j = 0; j < KX; ++j) {
+            if (l_n[j]) {
+                if (l_dst[j] + 4 <= cap) {
+                    *(uint32_u*)(o + l_dst[j]) = l_val[j];
+                } else {
+#pragma unroll
+                    for (uint32_t b = 0; b < 4; ++b)
+                        if (b < l_n[j]) o[l_dst[j] + b] = (uint8_t)(l_val[j] >> (8 * b));
                 }
-                // cpat_st == 1 cannot be seen here: the pattern is built in the
-                // memory section that follows the one that requested it
-            } else {
-                ld = true;
-                src = (int32_t)cq - (int32_t)cdist;
-                csz = C;
-                cdst = cq;
-                const uint32_t adv = C < crem ? C : crem;
-                cq += adv;
-                crem -= adv;
             }
-            if (ld) {
-                // 16 (32) bytes from src: the bytes used all lie in [src, cq);
-                // the rest may run into the next slot (never stored)
-                cw = *(const uint4_u*)(o + src);
-                if (C >= 32) cw2 = *(const uint4_u*)(o + src + 16);
-                cst = true;
+            if (m_sz[j]) {
+                uint4 w = m_w[j];
+                if (m_pat[j]) {
+                    // the cpd bytes before the match, repeated with period cpd
+                    const uint32_t cpd = m_pat[j] & 0xffu, csh = m_pat[j] >> 8;
+                    uint64_t v = ((uint64_t)w.y << 32) | w.x;
+                    v >>= 8 * csh;
+                    v &= (1ull << (8 * cpd)) - 1;
+                    if (cpd < 8) v |= v << (8 * cpd);
+                    if (cpd < 4) v |= v << (16 * cpd);
+                    if (cpd < 2) v |= v << (32 * cpd);
+                    if (cpat_st == 1) {   // still the current match
+                        cpat = v;
+                        cpat_st = 2;
+                    }
+                    w = make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0, 0);
+                }
+                store_bounded(o, m_dst[j], m_sz[j], cap, w);
             }
+            l_n[j] = 0;
+            m_sz[j] = 0;
+            m_pat[j] = 0;
         }
-        // ================================================ next token
-        if (!exited && crem == 0) {
+        // ================================================ take pieces
+        if (!exited) {
             const uint32_t head = lds_load(T + O_HEAD);
             compiler_fence();
-            uint2 e = make_uint2(0, 0);
-            if (tail != head) {
-                e = *(const uint2*)(T + ring_at(tail));
-                compiler_fence();
-            }
-            // a NEW token switches the output slot: the previous message's
-            // pending stores go out first
-            if (tail != head && !((e.y & TOK_NEW) && (cst || bcnt != 0))) {
-                ++tail;
-                lds_store(T + O_TAIL, tail);
-                worked = true;
-                if (e.y & TOK_END) {
-                    out_len[m] = e.x;
-                    status[m] = (int32_t)(int8_t)(e.y & 0xffu);
-                    done = true;
-                    exited = !queue;
-                } else if (e.y & TOK_NEW) {
-                    m = e.x;
-                    slot(m);
-                    pos = 0;
-                    done = false;
-                } else if (e.y & TOK_EXIT) {
-                    exited = true;
-                } else {
-                    const uint32_t nl = e.y & 7u, ml = (e.y >> 3) & 511u;
-                    if (nl) {
-                        bcnt = nl;
-                        bdst = pos;
-                        bval = e.x;
-                        pos += nl;
+            uint2 ent[KX];
+#pragma unroll
+            for (int j = 0; j < KX; ++j) ent[j] = *(const uint2*)(T + ring_at(tail + j));
+            compiler_fence();
+            const uint32_t F = crem ? cq : pos;   // everything before F is stored
+            uint32_t k = 0;                       // entries taken this iteration
+            bool stop = false;
+#pragma unroll
+            for (int j = 0; j < KX; ++j) {
+                if (!stop && crem == 0) {
+                    if (tail == head) {
+                        stop = true;
+                    } else {
+                        uint2 e = ent[0];
+#pragma unroll
+                        for (int i = 1; i <= j; ++i) e = k == (uint32_t)i ? ent[i] : e;
+                        if (e.y & TOK_END) {
+                            out_len[m] = e.x;
+                            const int32_t stt = (int32_t)(int8_t)(e.y & 0xffu);
+                            status[m] = stt;
+                            exited = !queue;
+                            ++tail;
+                            ++k;
+                            worked = true;
+                            stop = true;
+                        } else if (e.y & (TOK_NEW | TOK_EXIT)) {
+                            // switches the output slot: only with no piece pending
+                            if (j == 0) {
+                                if (e.y & TOK_NEW) {
+                                    m = e.x;
+                                    slot(m);
+                                    pos = 0;
+                                } else {
+                                    exited = true;
+                                }
+                                ++tail;
+                                ++k;
+                                worked = true;
+                            }
+                            stop = true;
+                        } else {
+                            const uint32_t nl = e.y & 7u, ml = (e.y >> 3) & 511u;
+                            if (nl) {
+                                l_dst[j] = pos;
+                                l_val[j] = e.x;
+                                l_n[j] = nl;
+                                pos += nl;
+                            }
+                            if (ml) {
+                                crem = ml;
+                                cdist = (e.y >> 12) & 0xffffu;
+                                cq = pos;
+                                cpat_st = 0;
+                                pos += ml;
+                            }
+                            ++tail;
+                            ++k;
+                            worked = true;
+                        }
                     }
-                    if (ml) {
-                        crem = ml;
-                        cdist = (e.y >> 12) & 0xffffu;
-                        cq = pos;
-                        cpat_st = 0;
-                        pos += ml;
+                }
+                if (!stop && crem != 0) {
+                    if (cdist >= 8) {
+                        // a chunk whose source lies below F: loaded now, stored next iteration
+                        const uint32_t C = cdist >= 16 ? 16u : 8u;
+                        const uint32_t n = crem < C ? crem : C;
+                        const int32_t src = (int32_t)cq - (int32_t)cdist;
+                        if (src + (int32_t)n <= (int32_t)F) {
+                            if (C == 16) {
+                                m_w[j] = *(const uint4_u*)(o + src);
+                            } else {
+                                const uint2 v = *(const uint2_u*)(o + src);
+                                m_w[j] = make_uint4(v.x, v.y, 0, 0);
+                            }
+                            m_dst[j] = cq;
+                            m_sz[j] = C;
+                            cq += n;
+                            crem -= n;
+                            worked = true;
+                        } else {
+                            stop = true;
+                        }
+                    } else {
+                        const uint32_t adv0 = 8 - 8 % cdist;
+                        const uint32_t adv = adv0 < crem ? adv0 : crem;
+                        if (cpat_st == 2) {
+                            m_w[j] = make_uint4((uint32_t)cpat, (uint32_t)(cpat >> 32), 0, 0);
+                            m_dst[j] = cq;
+                            m_sz[j] = 8;
+                            cq += adv;
+                            crem -= adv;
+                            worked = true;
+                        } else if (cpat_st == 0 && cq <= F) {
+                            // the cdist bytes before cq, read as 8 bytes that never
+                            // start before the slot's window
+                            const int32_t src = max((int32_t)cq - 8, -(int32_t)hist);
+                            const uint2 v = *(const uint2_u*)(o + src);
+                            m_w[j] = make_uint4(v.x, v.y, 0, 0);
+                            m_pat[j] = cdist | ((uint32_t)((int32_t)cq - (int32_t)cdist - src) << 8);
+                            cpat_st = 1;
+                            m_dst[j] = cq;
+                            m_sz[j] = 8;
+                            cq += adv;
+                            crem -= adv;
+                            worked = true;
+                        } else {
+                            stop = true;
+                        }
                     }
                 }
             }
+            lds_store(T + O_TAIL, tail);
         }
         if (!__ballot(worked)) {   // the decoder is behind: leave it the SIMD
             L3_CNT(2);

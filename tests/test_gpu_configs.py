@@ -28,7 +28,10 @@ def _c4(n=8192):
     return synth.make_batch("json", lens, seed=0x5EED0004)
 
 
-def _c5(n=512):
+def _c5(n=2048):
+    # 2048 messages: automatic mode sends them block-parallel, as the bench's
+    # C5 batch (inflate_impl: batches of 2048 - 32 Ki messages, payloads over
+    # 4 KiB compressed)
     lens = np.full(n, 65536, dtype=np.uint32)
     return synth.make_batch("binary", lens, seed=0x5EED0005)
 
@@ -137,13 +140,14 @@ def test_c4_work_queue_batch():
             pmd.lib().bpmd_set_inflate_kernel(0)
 
 
-def test_c4_long_payloads_split_to_wave_kernel():
-    """A work-queue batch whose longest payloads exceed twice the batch's
-    compressed bytes per resident lane (and 4 KiB): those are decoded by the
-    wave kernel from the longest-first order while the lane kernel takes the
-    rest (pmd_capi.hip inflate_impl, bpmd_internal_lane_long_split).  Every
-    message -- including corrupted long and short ones -- must equal the
-    oracle's inflate in status and bytes."""
+def test_c4_long_payloads_split_from_lanes():
+    """A work-queue batch whose longest payloads exceed half the batch's
+    compressed bytes per resident lane (and 2 KiB): those are decoded
+    block-parallel (pmd_inflate_bp.hip) on a side stream from the
+    longest-first order while the lane kernel takes the rest (pmd_capi.hip
+    inflate_impl, bpmd_internal_lane_long_split; the wave kernel when
+    BPMD_INFLATE_BP=0).  Every message -- including corrupted long and short
+    ones -- must equal the oracle's inflate in status and bytes."""
     import torch
     from beast_amd import pmd
     n = 70000
@@ -174,3 +178,40 @@ def test_c4_long_payloads_split_to_wave_kernel():
         a, b = int(o_off[i]), int(exp_off[i])
         k = int(exp_len[i])
         assert np.array_equal(outs[a:a + k], exp_out[b:b + k]), i
+
+
+def _full_roundtrip(kind, lens, seed, level):
+    """The bench's own mixed-leg path at the bench's own size: the whole batch
+    synthesized with the bench's seed, deflated on the GPU, inflated on the GPU
+    in automatic mode (lanes + block-parallel side stream), compared with the
+    original bytes on the device."""
+    import torch
+    from beast_amd import pmd
+    data, off, ln = synth.make_batch(kind, lens, seed=seed)
+    dev = torch.device("cuda", 0)
+    src = pmd.Batch(torch.from_numpy(data).to(dev), torch.from_numpy(off.astype(np.int64)).to(dev),
+                    torch.from_numpy(ln.astype(np.int32)).to(dev))
+    d = pmd.deflate_batch(src, level=level, mem_level=4)
+    torch.cuda.synchronize()
+    assert int((d.status != 0).sum()) == 0
+    cap = torch.from_numpy(ln.astype(np.int32)).to(dev)
+    # output slots laid out as the input batch, so the whole buffer compares
+    r = pmd.inflate_batch(pmd.Batch(d.out.data, d.out.off, d.out.len), cap, out_off=src.off)
+    torch.cuda.synchronize()
+    assert int((r.status != 0).sum()) == 0, np.nonzero(r.status.cpu().numpy())[0][:8]
+    assert torch.equal(r.out.len, cap)
+    assert torch.equal(r.out.data[: src.data.numel()], src.data)
+    return int(d.out.len.sum()) / float(ln.astype(np.float64).sum())
+
+
+def test_full_c4_batch_roundtrip():
+    """configs[3] at full size: 1 Mi Zipf JSON messages (8.4 GiB), L6."""
+    ratio = _full_roundtrip("json", synth.zipf_sizes(1 << 20, 0x5EED0004), 0x5EED0004, 6)
+    assert 0.2 < ratio < 0.4
+
+
+@pytest.mark.parametrize("level", [1, 6])
+def test_full_c5_batch_roundtrip(level):
+    """configs[4] at full size: 16 Ki x 64 KiB binary messages (1 GiB), L1 / L6."""
+    ratio = _full_roundtrip("binary", np.full(16384, 65536, dtype=np.uint32), 0x5EED0005, level)
+    assert 0.9 < ratio < 1.01
