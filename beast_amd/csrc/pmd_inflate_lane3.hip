@@ -80,6 +80,12 @@ constexpr uint32_t TOK_STORED = 0x10000000u;  // segment mode: bits 0-15 stored 
 #ifndef BPMD3_KX
 #define BPMD3_KX 4
 #endif
+#ifndef BPMD3_XSTEPS
+#define BPMD3_XSTEPS 1
+#endif
+#ifndef BPMD3_XPIPE
+#define BPMD3_XPIPE 0
+#endif
 constexpr int KX = BPMD3_KX;   // expander pieces per iteration
 #ifndef BPMD3_DPRIO
 #define BPMD3_DPRIO 3
@@ -389,6 +395,11 @@ __device__ __forceinline__ void expander_seg(uint8_t* T, bool valid, uint32_t m,
                                              bool queue, const uint8_t* __restrict__ in,
                                              const uint64_t* __restrict__ in_off, const uint32_t* __restrict__ in_len)
 {
+    // The batched pipeline of expander(): up to KX pieces per iteration, a
+    // piece being a token's literal symbols and one chunk -- of a match (8 or
+    // 16 symbols whose source lies below F or before the segment), of its
+    // pattern (distances below 8), or of a stored block's bytes (32, read from
+    // the payload) -- loaded in one iteration and stored in the next.
     uint16_t* o = sym;
     uint32_t cap = 0;
     const uint8_t* pl = in;   // the task's payload, [pl, pl_end)
@@ -402,176 +413,218 @@ __device__ __forceinline__ void expander_seg(uint8_t* T, bool valid, uint32_t m,
         pl_end = pl + in_len[mm];
     };
     if (valid) slot(m);
-    bool done = !valid;
-    bool exited = !queue && done;
+    bool exited = !queue && !valid;
     uint32_t tail = 0, pos = 0;
     uint32_t crem = 0, cdist = 0, cq = 0;
     uint4 cpat = make_uint4(0, 0, 0, 0);
-    uint32_t cpat_st = 0;   // dist < 8: 0 pattern not requested, 1 source in flight, 2 pattern ready
-    bool cst = false, cst_pat = false;
-    uint32_t cdst = 0, csz = 0, cpd = 1;
-    int32_t csrc = 0;
-    uint4 cw = make_uint4(0, 0, 0, 0), cw2 = cw;
-    uint32_t bcnt = 0, bdst = 0, bval = 0;
-    // stored block: bytes left, next source, next symbol; a loaded piece
-    // (up to 32 bytes) is stored in the next memory section
-    uint32_t srem = 0, sdst = 0, sp_dst = 0;
+    uint32_t cpat_st = 0;   // dist < 8: 0 pattern not requested, 1 requested, 2 ready
+    // stored block being copied: bytes left, next source, next symbol
+    uint32_t srem = 0, sdst = 0;
     const uint8_t* ssrc = in;
-    bool sp = false;
-    uint4 sw0 = make_uint4(0, 0, 0, 0), sw1 = sw0;
-    for (;;) {
-        const bool alive = !exited || crem != 0 || cst || bcnt != 0 || srem != 0 || sp;
-        if (!__ballot(alive)) break;
-        bool worked = cst || bcnt != 0 || crem != 0 || srem != 0 || sp;
-        // ================================================ memory section
-        if (sp) {
-            store_syms8(o, sp_dst, cap, make_uint4(sym_lo(sw0.x), sym_hi(sw0.x), sym_lo(sw0.y), sym_hi(sw0.y)));
-            store_syms8(o, sp_dst + 8, cap, make_uint4(sym_lo(sw0.z), sym_hi(sw0.z), sym_lo(sw0.w), sym_hi(sw0.w)));
-            store_syms8(o, sp_dst + 16, cap, make_uint4(sym_lo(sw1.x), sym_hi(sw1.x), sym_lo(sw1.y), sym_hi(sw1.y)));
-            store_syms8(o, sp_dst + 24, cap, make_uint4(sym_lo(sw1.z), sym_hi(sw1.z), sym_lo(sw1.w), sym_hi(sw1.w)));
-            sp = false;
-        }
-        if (srem) {
-            const uint32_t k = srem < 32 ? srem : 32u;
-            if (ssrc + 32 <= pl_end) {
-                sw0 = *(const uint4_u*)ssrc;
-                sw1 = *(const uint4_u*)(ssrc + 16);
-            } else {
-                // the payload's last bytes: nothing past its end is read
-                uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-                for (uint32_t j = 0; j < k; ++j) d[j >> 2] |= (uint32_t)ssrc[j] << (8 * (j & 3));
-                sw0 = make_uint4(d[0], d[1], d[2], d[3]);
-                sw1 = make_uint4(d[4], d[5], d[6], d[7]);
-            }
-            sp = true;
-            sp_dst = sdst;
-            ssrc += k;
-            sdst += k;
-            srem -= k;
-        }
-        if (cst) {
-            uint4 w = ref_fix(cw, csrc);
-            if (cst_pat) {
-                w = sym_pattern(w, cpd);
-                if (cpat_st == 1) {   // still the current match
-                    cpat = w;
-                    cpat_st = 2;
-                }
-            }
-            store_syms8(o, cdst, cap, w);
-            if (csz == 16) store_syms8(o, cdst + 8, cap, ref_fix(cw2, csrc + 8));
-            cst = false;
-            cst_pat = false;
-        }
-        if (bcnt) {
-            // the token's literal bytes as four symbols, one 8-byte store
-            const uint2 w = make_uint2((bval & 0xffu) | ((bval & 0xff00u) << 8),
-                                       ((bval >> 16) & 0xffu) | ((bval >> 8) & 0xff0000u));
-            if (bdst + 4 <= cap) {
-                *(uint2_s*)(o + bdst) = w;
-            } else {
+    // pieces: literal symbols, and a chunk of kind 0 none, 1 match, 2 pattern
+    // (ready), 3 pattern request, 4 stored bytes
+    constexpr uint32_t CK_MATCH = 1, CK_PAT = 2, CK_PATREQ = 3, CK_STORED = 4;
+    uint32_t l_dst[KX], l_val[KX], l_n[KX], c_kind[KX], c_dst[KX], c_sz[KX];
+    int32_t c_src[KX];
+    uint4 c_w0[KX], c_w1[KX];
 #pragma unroll
-                for (uint32_t j = 0; j < 4; ++j)
-                    if (j < bcnt && bdst + j < cap) o[bdst + j] = (uint16_t)((bval >> (8 * j)) & 0xffu);
-            }
-            bcnt = 0;
-        }
-        if (crem) {
-            const uint32_t C = (cdist >= 16 && crem > 8) ? 16u : cdist >= 8 ? 8u : 0u;
-            bool ld = false;
-            int32_t src = 0;
-            if (C == 0) {
-                const uint32_t adv0 = 8 - 8 % cdist;
-                const uint32_t adv = adv0 < crem ? adv0 : crem;
-                if (cpat_st == 2) {
-                    store_syms8(o, cq, cap, cpat);
-                    cq += adv;
-                    crem -= adv;
-                } else if (cpat_st == 0) {
-                    ld = true;
-                    src = (int32_t)cq - 8;
-                    cst_pat = true;
-                    cpd = cdist;
-                    csz = 8;
-                    cpat_st = 1;
-                    cdst = cq;
-                    cq += adv;
-                    crem -= adv;
-                }
-            } else {
-                ld = true;
-                src = (int32_t)cq - (int32_t)cdist;
-                csz = C;
-                cdst = cq;
-                const uint32_t adv = C < crem ? C : crem;
-                cq += adv;
-                crem -= adv;
-            }
-            if (ld) {
-                cw = make_uint4(0, 0, 0, 0);
-                cw2 = cw;
-                if (src + 8 > 0) cw = *(const uint4_s*)(o + src);
-                if (csz == 16 && src + 16 > 0) cw2 = *(const uint4_s*)(o + src + 8);
-                csrc = src;
-                cst = true;
-            }
-        }
-        // ================================================ next token
-        if (!exited && crem == 0 && srem == 0) {
-            const uint32_t head = lds_load(T + O_HEAD);
-            compiler_fence();
-            uint2 e = make_uint2(0, 0);
-            if (tail != head) {
-                e = *(const uint2*)(T + ring_at(tail));
-                compiler_fence();
-            }
-            if (tail != head && !((e.y & TOK_NEW) && (cst || bcnt != 0 || sp))) {
-                ++tail;
-                lds_store(T + O_TAIL, tail);
-                worked = true;
-                if (e.y & TOK_END) {
-                    const uint32_t delta = (e.y >> 8) & 0x1fffffu;
-                    bp::SegRes r;
-                    r.nsym = e.x;
-                    r.status = (int32_t)(int8_t)(e.y & 0xffu);
-                    r.next = delta ? m + delta : 0xffffffffu;
-                    r.pad = 0;
-                    res[m] = r;
-                    done = true;
-                    exited = !queue;
-                } else if (e.y & TOK_NEW) {
-                    m = e.x;
-                    slot(m);
-                    pos = 0;
-                    done = false;
-                } else if (e.y & TOK_EXIT) {
-                    exited = true;
-                } else if (e.y & TOK_STORED) {
-                    srem = e.y & 0xffffu;
-                    ssrc = pl + e.x;
-                    sdst = pos;
-                    pos += srem;
+    for (int j = 0; j < KX; ++j) {
+        l_dst[j] = l_val[j] = l_n[j] = c_kind[j] = c_dst[j] = c_sz[j] = 0;
+        c_src[j] = 0;
+        c_w0[j] = c_w1[j] = make_uint4(0, 0, 0, 0);
+    }
+    for (;;) {
+        bool pending = false;
+#pragma unroll
+        for (int j = 0; j < KX; ++j) pending = pending || l_n[j] != 0 || c_kind[j] != 0;
+        if (!__ballot(!exited || crem != 0 || srem != 0 || pending)) break;
+        bool worked = pending;
+        // ================================================ stores, output order
+#pragma unroll
+        for (int j = 0; j < KX; ++j) {
+            if (l_n[j]) {
+                // the token's literal bytes as four symbols, one 8-byte store
+                const uint32_t bval = l_val[j], bdst = l_dst[j];
+                const uint2 w = make_uint2((bval & 0xffu) | ((bval & 0xff00u) << 8),
+                                           ((bval >> 16) & 0xffu) | ((bval >> 8) & 0xff0000u));
+                if (bdst + 4 <= cap) {
+                    *(uint2_s*)(o + bdst) = w;
                 } else {
-                    const uint32_t nl = e.y & 7u, ml = (e.y >> 3) & 511u;
-                    if (nl) {
-                        bcnt = nl;
-                        bdst = pos;
-                        bval = e.x;
-                        pos += nl;
+#pragma unroll
+                    for (uint32_t q = 0; q < 4; ++q)
+                        if (q < l_n[j] && bdst + q < cap) o[bdst + q] = (uint16_t)((bval >> (8 * q)) & 0xffu);
+                }
+            }
+            if (c_kind[j] == CK_STORED) {
+                const uint4 w0 = c_w0[j], w1 = c_w1[j];
+                const uint32_t d = c_dst[j];
+                store_syms8(o, d, cap, make_uint4(sym_lo(w0.x), sym_hi(w0.x), sym_lo(w0.y), sym_hi(w0.y)));
+                store_syms8(o, d + 8, cap, make_uint4(sym_lo(w0.z), sym_hi(w0.z), sym_lo(w0.w), sym_hi(w0.w)));
+                store_syms8(o, d + 16, cap, make_uint4(sym_lo(w1.x), sym_hi(w1.x), sym_lo(w1.y), sym_hi(w1.y)));
+                store_syms8(o, d + 24, cap, make_uint4(sym_lo(w1.z), sym_hi(w1.z), sym_lo(w1.w), sym_hi(w1.w)));
+            } else if (c_kind[j] == CK_PAT) {
+                store_syms8(o, c_dst[j], cap, c_w0[j]);
+            } else if (c_kind[j]) {
+                uint4 w = ref_fix(c_w0[j], c_src[j]);
+                if (c_kind[j] == CK_PATREQ) {
+                    w = sym_pattern(w, c_sz[j]);
+                    if (cpat_st == 1) {   // still the current match
+                        cpat = w;
+                        cpat_st = 2;
                     }
-                    if (ml) {
-                        crem = ml;
-                        cdist = (e.y >> 12) & 0xffffu;
-                        cq = pos;
-                        cpat_st = 0;
-                        pos += ml;
+                }
+                store_syms8(o, c_dst[j], cap, w);
+                if (c_kind[j] == CK_MATCH && c_sz[j] == 16) store_syms8(o, c_dst[j] + 8, cap, ref_fix(c_w1[j], c_src[j] + 8));
+            }
+            l_n[j] = 0;
+            c_kind[j] = 0;
+        }
+        // ================================================ take pieces
+        if (!exited || crem != 0 || srem != 0) {
+            const uint32_t head = exited ? tail : lds_load(T + O_HEAD);
+            compiler_fence();
+            uint2 ent[KX];
+#pragma unroll
+            for (int j = 0; j < KX; ++j) ent[j] = *(const uint2*)(T + ring_at(tail + j));
+            compiler_fence();
+            const uint32_t F = crem ? cq : srem ? sdst : pos;   // every symbol before F is stored
+            uint32_t k = 0;
+            bool stop = false;
+#pragma unroll
+            for (int j = 0; j < KX; ++j) {
+                if (!stop && crem == 0 && srem == 0) {
+                    if (tail == head) {
+                        stop = true;
+                    } else {
+                        uint2 e = ent[0];
+#pragma unroll
+                        for (int i = 1; i <= j; ++i) e = k == (uint32_t)i ? ent[i] : e;
+                        if (e.y & TOK_END) {
+                            const uint32_t delta = (e.y >> 8) & 0x1fffffu;
+                            bp::SegRes r;
+                            r.nsym = e.x;
+                            r.status = (int32_t)(int8_t)(e.y & 0xffu);
+                            r.next = delta ? m + delta : 0xffffffffu;
+                            r.pad = 0;
+                            res[m] = r;
+                            exited = !queue;
+                            ++tail;
+                            ++k;
+                            worked = true;
+                            stop = true;
+                        } else if (e.y & (TOK_NEW | TOK_EXIT)) {
+                            if (j == 0) {   // switches the slot: only with no piece pending
+                                if (e.y & TOK_NEW) {
+                                    m = e.x;
+                                    slot(m);
+                                    pos = 0;
+                                } else {
+                                    exited = true;
+                                }
+                                ++tail;
+                                ++k;
+                                worked = true;
+                            }
+                            stop = true;
+                        } else if (e.y & TOK_STORED) {
+                            srem = e.y & 0xffffu;
+                            ssrc = pl + e.x;
+                            sdst = pos;
+                            pos += srem;
+                            ++tail;
+                            ++k;
+                            worked = true;
+                        } else {
+                            const uint32_t nl = e.y & 7u, ml = (e.y >> 3) & 511u;
+                            if (nl) {
+                                l_dst[j] = pos;
+                                l_val[j] = e.x;
+                                l_n[j] = nl;
+                                pos += nl;
+                            }
+                            if (ml) {
+                                crem = ml;
+                                cdist = (e.y >> 12) & 0xffffu;
+                                cq = pos;
+                                cpat_st = 0;
+                                pos += ml;
+                            }
+                            ++tail;
+                            ++k;
+                            worked = true;
+                        }
+                    }
+                }
+                if (!stop && srem != 0) {
+                    // 32 stored bytes (nothing past the payload's end is read)
+                    const uint32_t kb = srem < 32 ? srem : 32u;
+                    if (ssrc + 32 <= pl_end) {
+                        c_w0[j] = *(const uint4_u*)ssrc;
+                        c_w1[j] = *(const uint4_u*)(ssrc + 16);
+                    } else {
+                        uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                        for (uint32_t q = 0; q < kb; ++q) d[q >> 2] |= (uint32_t)ssrc[q] << (8 * (q & 3));
+                        c_w0[j] = make_uint4(d[0], d[1], d[2], d[3]);
+                        c_w1[j] = make_uint4(d[4], d[5], d[6], d[7]);
+                    }
+                    c_kind[j] = CK_STORED;
+                    c_dst[j] = sdst;
+                    ssrc += kb;
+                    sdst += kb;
+                    srem -= kb;
+                    worked = true;
+                } else if (!stop && crem != 0) {
+                    const uint32_t C = (cdist >= 16 && crem > 8) ? 16u : cdist >= 8 ? 8u : 0u;
+                    if (C) {
+                        const uint32_t n = crem < C ? crem : C;
+                        const int32_t src = (int32_t)cq - (int32_t)cdist;
+                        if (src + (int32_t)n <= (int32_t)F) {
+                            uint4 w0 = make_uint4(0, 0, 0, 0), w1 = w0;
+                            if (src + 8 > 0) w0 = *(const uint4_s*)(o + src);
+                            if (C == 16 && src + 16 > 0) w1 = *(const uint4_s*)(o + src + 8);
+                            c_w0[j] = w0;
+                            c_w1[j] = w1;
+                            c_src[j] = src;
+                            c_kind[j] = CK_MATCH;
+                            c_dst[j] = cq;
+                            c_sz[j] = C;
+                            cq += n;
+                            crem -= n;
+                            worked = true;
+                        } else {
+                            stop = true;
+                        }
+                    } else {
+                        const uint32_t adv0 = 8 - 8 % cdist;
+                        const uint32_t adv = adv0 < crem ? adv0 : crem;
+                        if (cpat_st == 2) {
+                            c_w0[j] = cpat;
+                            c_kind[j] = CK_PAT;
+                            c_dst[j] = cq;
+                            cq += adv;
+                            crem -= adv;
+                            worked = true;
+                        } else if (cpat_st == 0 && cq <= F) {
+                            const int32_t src = (int32_t)cq - 8;
+                            c_w0[j] = src + 8 > 0 ? *(const uint4_s*)(o + src) : make_uint4(0, 0, 0, 0);
+                            c_src[j] = src;
+                            c_kind[j] = CK_PATREQ;
+                            c_sz[j] = cdist;   // the pattern's period
+                            c_dst[j] = cq;
+                            cpat_st = 1;
+                            cq += adv;
+                            crem -= adv;
+                            worked = true;
+                        } else {
+                            stop = true;
+                        }
                     }
                 }
             }
+            if (!exited || k) lds_store(T + O_TAIL, tail);
         }
         if (!__ballot(worked)) __builtin_amdgcn_s_sleep(BPMD3_ESLEEP);
     }
-    (void)done;
 }
 
 // ------------------------------------------------------------------- decoder
@@ -1387,7 +1440,10 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
         // publish and the wave's exit tests -- is then paid once per two
         // tokens (about half of the data lanes take it; a
         // third step, or refilling the input block first, measured neutral).
-        if (__ballot(st0 == S_DATA && st == S_DATA && !nx_used && head - taken < RING)) {
+#pragma unroll
+        for (int xs = 0; xs < BPMD3_XSTEPS; ++xs) {
+            if (BPMD3_XPIPE && nx_used && st0 == S_DATA && st == S_DATA) pipe();
+            if (!__ballot(st0 == S_DATA && st == S_DATA && !nx_used && head - taken < RING)) break;
             uint32_t enl2 = 0, elit2 = 0, emlen2 = 0, edist2 = 0;
             if (st0 == S_DATA && st == S_DATA && !nx_used && head - taken < RING)
                 data_step(enl2, elit2, emlen2, edist2);
