@@ -37,13 +37,7 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
                                         uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                                         uint32_t* out_len, int32_t* status, uint32_t raw, const uint32_t* order,
                                         const uint32_t* nlong, hipStream_t s);
-extern "C" int bpmd_internal_inflate_bp_plan(const uint32_t* in_len, uint32_t n, const uint32_t* out_cap,
-                                             const uint32_t* order, const uint32_t* nlong, hipStream_t s,
-                                             uint64_t* ntask_out);
-extern "C" int bpmd_internal_inflate_bp_run(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
-                                            uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
-                                            uint32_t* out_len, int32_t* status, uint32_t raw, const uint32_t* order,
-                                            const uint32_t* nlong, hipStream_t s);
+extern "C" void bpmd_internal_bp_release(hipStream_t s);
 extern "C" int bpmd_internal_inflate_wave_ordered(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                                   uint32_t n, uint8_t* out, const uint64_t* out_off,
                                                   const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
@@ -199,8 +193,10 @@ extern "C" void bpmd_internal_scratch_release(hipStream_t s)
 {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return;
-    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    bpmd_internal_bp_release(s);
     hipStream_t side = nullptr;
+    {
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
     for (size_t i = 0; i < g_sides.size(); ++i)
         if (g_sides[i].dev == dev && g_sides[i].stream == s) {
             side = g_sides[i].side;
@@ -227,7 +223,11 @@ extern "C" void bpmd_internal_scratch_release(hipStream_t s)
             g_locks.pop_back();
             break;
         }
-    if (side) (void)hipStreamDestroy(side);
+    }
+    if (side) {
+        bpmd_internal_bp_release(side);
+        (void)hipStreamDestroy(side);
+    }
 }
 
 // Number of scratch blocks held (footprint tests)
@@ -410,16 +410,12 @@ int inflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
                     if (!side_for(s, sd) || hipEventRecord(sd.fork, s) != hipSuccess ||
                         hipStreamWaitEvent(sd.side, sd.fork, 0) != hipSuccess)
                         return BPMD_R_HIP_ERROR;
-                    // the plan's read-back goes first, while the chip is idle
-                    // (behind the lane kernel it would wait for a free CU)
-                    uint64_t ntask = 0;
-                    int eb = bpmd_internal_inflate_bp_plan(d_in_len, n_msgs, d_out_cap, order, nlong, sd.side, &ntask);
+                    // (both enqueue only: nothing here waits on the device)
+                    const int eb = bpmd_internal_inflate_bp(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off,
+                                                            d_out_cap, d_out_len, d_status, raw, order, nlong, sd.side);
                     e = bpmd_internal_inflate_lane3(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap,
                                                     d_out_len, d_status, raw, key, hist, 1u << cfg->window_bits, 0u,
                                                     order, qctr, wgs, nlong, s);
-                    if (!eb && ntask)
-                        eb = bpmd_internal_inflate_bp_run(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_cap,
-                                                          d_out_len, d_status, raw, order, nlong, sd.side);
                     if (hipEventRecord(sd.join, sd.side) != hipSuccess || hipStreamWaitEvent(s, sd.join, 0) != hipSuccess)
                         return BPMD_R_HIP_ERROR;
                     return e || eb ? BPMD_R_HIP_ERROR : BPMD_R_OK;

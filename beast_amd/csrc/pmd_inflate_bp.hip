@@ -44,6 +44,9 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <mutex>
+#include <vector>
+
 #include "bp.h"
 #include "canon.h"
 #include "pmd_common.h"
@@ -51,7 +54,8 @@
 extern "C" void* bpmd_internal_scratch(hipStream_t s, size_t bytes, int which);
 extern "C" int bpmd_internal_inflate_lane3_seg(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                                uint32_t n_tasks, const void* tasks, uint16_t* sym, void* res,
-                                               uint32_t raw, uint32_t* qctr, uint32_t grid_wgs, hipStream_t stream);
+                                               uint32_t raw, uint32_t* qctr, uint32_t grid_wgs, hipStream_t stream,
+                                               const uint32_t* n_dev);
 extern "C" int bpmd_internal_inflate_wave_ordered(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                                   uint32_t n, uint8_t* out, const uint64_t* out_off,
                                                   const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
@@ -140,6 +144,39 @@ __global__ void bp_totals_kernel(const uint32_t* __restrict__ regions, const uin
         tot->tasks = (unsigned long long)task_base[n - 1] + regions[n - 1];
         tot->words = word_base[n - 1] + words[n - 1];
     }
+}
+
+// Without a read-back the decode workspace has a fixed capacity (tasks,
+// symbol words): the long payloads that fit are a prefix of the order
+// (the sums only grow), the rest go to the wave kernel's list.  fit[0] =
+// payloads decoded block-parallel, fit[1] = their tasks; *tot = the totals
+// the whole list would need (the host grows the capacity from them).
+__global__ void __launch_bounds__(256)
+bp_fit_kernel(const uint32_t* __restrict__ nlong, const uint32_t* __restrict__ regions,
+              const uint32_t* __restrict__ task_base, const unsigned long long* __restrict__ words,
+              const unsigned long long* __restrict__ word_base, uint32_t n, unsigned long long cap_tasks,
+              unsigned long long cap_words, const uint32_t* __restrict__ order, uint32_t* __restrict__ fit,
+              Totals* __restrict__ tot, uint32_t* __restrict__ fb_list, uint32_t* __restrict__ fb_count)
+{
+    const uint32_t nl = *nlong < n ? *nlong : n;
+    auto fits = [&](uint32_t k) {   // the first k payloads fit
+        return k == 0 || ((unsigned long long)task_base[k - 1] + regions[k - 1] <= cap_tasks &&
+                          word_base[k - 1] + words[k - 1] <= cap_words);
+    };
+    uint32_t lo = 0, hi = nl;   // largest k <= nl with fits(k)
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (fits(mid)) lo = mid;
+        else hi = mid - 1;
+    }
+    const uint32_t nfit = lo;
+    if (threadIdx.x == 0) {
+        fit[0] = nfit;
+        fit[1] = nfit ? task_base[nfit - 1] + regions[nfit - 1] : 0u;
+        tot->tasks = n ? (unsigned long long)task_base[n - 1] + regions[n - 1] : 0ull;
+        tot->words = n ? word_base[n - 1] + words[n - 1] : 0ull;
+    }
+    for (uint32_t i = nfit + threadIdx.x; i < nl; i += blockDim.x) fb_list[atomicAdd(fb_count, 1u)] = order[i];
 }
 
 // diagnostics (bpmd_diag_bp_counters): [0] payloads resolved, [1] segments
@@ -398,10 +435,12 @@ template <bool DYN>
 __global__ void __launch_bounds__(64 * SCAN_WAVES)
 bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                const uint32_t* __restrict__ in_len, const uint32_t* __restrict__ order,
-               const uint32_t* __restrict__ region_map, uint32_t n_regions, const Stat* __restrict__ stats,
-               const uint32_t* __restrict__ task_base, SegTask* __restrict__ tasks, uint32_t* __restrict__ marked)
+               const uint32_t* __restrict__ region_map, const uint32_t* __restrict__ n_regions_dev,
+               const Stat* __restrict__ stats, const uint32_t* __restrict__ task_base, SegTask* __restrict__ tasks,
+               uint32_t* __restrict__ marked)
 {
     __shared__ ScanLds L;
+    const uint32_t n_regions = *n_regions_dev;
     for (uint32_t f = threadIdx.x; f < 4096; f += blockDim.x) L.kraft[f] = (uint16_t)kraft4(f);
     __syncthreads();
     const uint32_t lane = wave_lane(), wv = threadIdx.x >> 6;
@@ -837,49 +876,84 @@ bp_resolve_kernel(const uint32_t* __restrict__ order, const uint32_t* __restrict
 // ------------------------------------------------------------------ driver
 // Long payloads order[0, *nlong) of a batch (pmd_capi.hip inflate_impl); the
 // rest of the batch is the caller's.  n: the batch's message count (bounds
-// nlong).  Returns 0 or a HIP error; *used = 0 when there was nothing to do.
+// nlong).  Everything is enqueued on s and nothing waits on the device: the
+// decode workspace has a per-(device, stream) capacity, the long payloads
+// that do not fit it go to the wave kernel (bp_fit_kernel), and each call's
+// totals are copied to pinned memory so that a later call grows the capacity
+// to them (the growth itself frees the old block only once s is idle).
 namespace {
-struct BpHost {
-    bpmd::bp::Totals* tot = nullptr;   // pinned
-    hipEvent_t ev = nullptr;
-};
-BpHost& bp_host()
-{
-    thread_local BpHost h;
-    if (!h.tot) {
-        if (hipHostMalloc((void**)&h.tot, sizeof(bpmd::bp::Totals), hipHostMallocDefault) != hipSuccess) h.tot = nullptr;
-        if (hipEventCreateWithFlags(&h.ev, hipEventDisableTiming) != hipSuccess) h.ev = nullptr;
-    }
-    return h;
-}
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+struct BpCaps {
+    int dev;
+    hipStream_t s;
+    unsigned long long tasks, words;   // decode workspace capacity
+    bpmd::bp::Totals* seen;            // pinned: the totals of the last call
+    hipEvent_t ev;                     // recorded after that copy
+    bool pending;
+};
+std::mutex g_bp_mu;
+std::vector<BpCaps> g_bp_caps;
+constexpr unsigned long long BP_TASKS0 = 1ull << 16, BP_WORDS0 = 1ull << 25;   // first capacity: 64 Ki tasks, 64 MiB
 }  // namespace
 
-// Phase 1 (plan): per-payload stats, the exclusive sums and one small
-// read-back of the totals to size the decode workspace; the host waits for
-// it, so a caller that overlaps other work launches that work after this.
-// Phase 2 (run): scan, slots, segment decode, resolve, fallback.  Both on s.
-struct BpPlan {
-    uint32_t n, cus;
-    uint64_t ntask, nword;
-    bpmd::bp::Stat* st;
-    uint32_t *reg, *tbase, *q;
-    unsigned long long* wbase;
-};
-thread_local BpPlan g_plan;
+// frees the pinned totals and event of a stream about to be destroyed
+extern "C" void bpmd_internal_bp_release(hipStream_t s)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return;
+    std::lock_guard<std::mutex> lk(g_bp_mu);
+    for (size_t i = 0; i < g_bp_caps.size(); ++i)
+        if (g_bp_caps[i].dev == dev && g_bp_caps[i].s == s) {
+            (void)hipEventSynchronize(g_bp_caps[i].ev);
+            (void)hipHostFree(g_bp_caps[i].seen);
+            (void)hipEventDestroy(g_bp_caps[i].ev);
+            g_bp_caps[i] = g_bp_caps.back();
+            g_bp_caps.pop_back();
+            return;
+        }
+}
 
-extern "C" int bpmd_internal_inflate_bp_plan(const uint32_t* in_len, uint32_t n, const uint32_t* out_cap,
-                                             const uint32_t* order, const uint32_t* nlong, hipStream_t s,
-                                             uint64_t* ntask_out)
+extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n,
+                                        uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                                        uint32_t* out_len, int32_t* status, uint32_t raw, const uint32_t* order,
+                                        const uint32_t* nlong, hipStream_t s)
 {
     using namespace bpmd::bp;
-    *ntask_out = 0;
-    g_plan.ntask = 0;
     if (n == 0) return 0;
-    BpHost& H = bp_host();
-    if (!H.tot || !H.ev) return (int)hipErrorOutOfMemory;
-    // stats workspace (scratch block 10): stats, regions, words, their
-    // exclusive sums, totals, scan temp
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    // this stream's capacity, grown to what an earlier call needed
+    unsigned long long cap_tasks = 0, cap_words = 0;
+    Totals* seen = nullptr;
+    hipEvent_t ev = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_bp_mu);
+        BpCaps* c = nullptr;
+        for (auto& e : g_bp_caps)
+            if (e.dev == dev && e.s == s) c = &e;
+        if (!c) {
+            BpCaps e{dev, s, BP_TASKS0, BP_WORDS0, nullptr, nullptr, false};
+            if (hipHostMalloc((void**)&e.seen, sizeof(Totals), hipHostMallocDefault) != hipSuccess)
+                return (int)hipErrorOutOfMemory;
+            if (hipEventCreateWithFlags(&e.ev, hipEventDisableTiming) != hipSuccess) return (int)hipErrorUnknown;
+            g_bp_caps.push_back(e);
+            c = &g_bp_caps.back();
+        }
+        if (c->pending && hipEventQuery(c->ev) == hipSuccess) {
+            c->pending = false;
+            const unsigned long long t = c->seen->tasks, w = c->seen->words;
+            if (t > c->tasks) c->tasks = t + t / 4;
+            if (w > c->words) c->words = w + w / 4;
+        }
+        if (c->tasks > 0xffffffffull) c->tasks = 0xffffffffull;
+        cap_tasks = c->tasks;
+        cap_words = c->words;
+        seen = c->seen;
+        ev = c->ev;
+        c->pending = true;
+    }
+    // per-payload workspace (scratch block 10): stats, regions, words, their
+    // exclusive sums, totals, fit, queues, scan temp
     size_t tmp1 = 0, tmp2 = 0;
     if (hipcub::DeviceScan::ExclusiveSum(nullptr, tmp1, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, s) !=
             hipSuccess ||
@@ -888,10 +962,19 @@ extern "C" int bpmd_internal_inflate_bp_plan(const uint32_t* in_len, uint32_t n,
         return (int)hipErrorUnknown;
     const size_t o_st = 0, o_reg = al256(o_st + sizeof(Stat) * (size_t)n), o_tb = al256(o_reg + 4ull * n),
                  o_w = al256(o_tb + 4ull * n), o_wb = al256(o_w + 8ull * n), o_tot = al256(o_wb + 8ull * n),
-                 o_q = al256(o_tot + sizeof(Totals)), o_tmp = al256(o_q + 64), sz = al256(o_tmp + (tmp1 > tmp2 ? tmp1 : tmp2));
-    // q: [0] scan queue, [1] resolve queue, [2] fallback count, [3] seg queue, [4-5] long bytes
+                 o_q = al256(o_tot + sizeof(Totals)), o_tmp = al256(o_q + 64),
+                 sz = al256(o_tmp + (tmp1 > tmp2 ? tmp1 : tmp2));
+    // q: [0] scan queue, [1] resolve queue, [2] fallback count, [3] seg queue,
+    // [4-5] long bytes, [6] payloads that fit, [7] their tasks
     uint8_t* ws = (uint8_t*)bpmd_internal_scratch(s, sz, 10);
-    if (!ws) return (int)hipErrorOutOfMemory;
+    // decode workspace (scratch block 11), sized by the capacity: tasks,
+    // results, fallback list, region map, marks, symbols
+    const size_t d_tasks = 0, d_res = al256(d_tasks + sizeof(SegTask) * cap_tasks),
+                 d_fb = al256(d_res + sizeof(SegRes) * cap_tasks), d_map = al256(d_fb + 4ull * n),
+                 d_mark = al256(d_map + 4ull * cap_tasks), d_sym = al256(d_mark + 4ull * n),
+                 dsz = al256(d_sym + 2ull * (cap_words + SYM_GUARD + 64));
+    uint8_t* dw = (uint8_t*)bpmd_internal_scratch(s, dsz, 11);
+    if (!ws || !dw) return (int)hipErrorOutOfMemory;
     Stat* st = (Stat*)(ws + o_st);
     uint32_t* reg = (uint32_t*)(ws + o_reg);
     uint32_t* tbase = (uint32_t*)(ws + o_tb);
@@ -900,10 +983,16 @@ extern "C" int bpmd_internal_inflate_bp_plan(const uint32_t* in_len, uint32_t n,
     Totals* dtot = (Totals*)(ws + o_tot);
     uint32_t* q = (uint32_t*)(ws + o_q);
     void* tmp = ws + o_tmp;
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    SegTask* tasks = (SegTask*)(dw + d_tasks);
+    SegRes* res = (SegRes*)(dw + d_res);
+    uint32_t* fb = (uint32_t*)(dw + d_fb);
+    uint16_t* sym = (uint16_t*)(dw + d_sym);
+    uint32_t* rmap = (uint32_t*)(dw + d_map);
+    uint32_t* marked = (uint32_t*)(dw + d_mark);
     unsigned long long* total = (unsigned long long*)(q + 4);
-    if (hipMemsetAsync(q, 0, 64, s) != hipSuccess) return (int)hipErrorUnknown;
+    uint32_t* fit = q + 6;
+    if (hipMemsetAsync(q, 0, 64, s) != hipSuccess || hipMemsetAsync(marked, 0, 4ull * n, s) != hipSuccess)
+        return (int)hipErrorUnknown;
     hipLaunchKernelGGL(bp_sum_kernel, dim3(n / 256 + 1 < 1024 ? n / 256 + 1 : 1024), dim3(256), 0, s, in_len, order,
                        nlong, n, total);
     // BPMD_BP_SEGS (diagnostics): target segments per lane of the chip
@@ -919,77 +1008,36 @@ extern "C" int bpmd_internal_inflate_bp_plan(const uint32_t* in_len, uint32_t n,
     if (hipcub::DeviceScan::ExclusiveSum(tmp, t1, reg, tbase, (int)n, s) != hipSuccess ||
         hipcub::DeviceScan::ExclusiveSum(tmp, t2, words, wbase, (int)n, s) != hipSuccess)
         return (int)hipErrorUnknown;
-    hipLaunchKernelGGL(bp_totals_kernel, dim3(1), dim3(64), 0, s, reg, tbase, words, wbase, n, dtot);
+    hipLaunchKernelGGL(bp_fit_kernel, dim3(1), dim3(256), 0, s, nlong, reg, tbase, words, wbase, n, cap_tasks,
+                       cap_words, order, fit, dtot, fb, q + 2);
+    // the totals for a later call (pinned, no wait here)
     if (hipGetLastError() != hipSuccess ||
-        hipMemcpyAsync(H.tot, dtot, sizeof(Totals), hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipEventRecord(H.ev, s) != hipSuccess || hipEventSynchronize(H.ev) != hipSuccess)
+        hipMemcpyAsync(seen, dtot, sizeof(Totals), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipEventRecord(ev, s) != hipSuccess)
         return (int)hipErrorUnknown;
-    if (H.tot->tasks > 0xffffffffull) return (int)hipErrorInvalidValue;
-    g_plan = BpPlan{n, (uint32_t)cus, H.tot->tasks, H.tot->words, st, reg, tbase, q, wbase};
-    *ntask_out = H.tot->tasks;
-    return 0;
-}
-
-extern "C" int bpmd_internal_inflate_bp_run(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
-                                            uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
-                                            uint32_t* out_len, int32_t* status, uint32_t raw, const uint32_t* order,
-                                            const uint32_t* nlong, hipStream_t s)
-{
-    using namespace bpmd::bp;
-    const BpPlan P = g_plan;
-    const uint64_t ntask = P.ntask, nword = P.nword;
-    if (ntask == 0) return 0;
-    const uint32_t n = P.n, cus = P.cus;
-    Stat* st = P.st;
-    uint32_t *reg = P.reg, *tbase = P.tbase, *q = P.q;
-    unsigned long long* wbase = P.wbase;
-    // decode workspace (scratch block 11): tasks, results, fallback list, symbols
-    const size_t d_tasks = 0, d_res = al256(d_tasks + sizeof(SegTask) * ntask), d_fb = al256(d_res + sizeof(SegRes) * ntask),
-                 d_map = al256(d_fb + 4ull * n), d_mark = al256(d_map + 4ull * ntask), d_sym = al256(d_mark + 4ull * n),
-                 dsz = al256(d_sym + 2ull * (nword + SYM_GUARD + 64));
-    uint8_t* dw = (uint8_t*)bpmd_internal_scratch(s, dsz, 11);
-    if (!dw) return (int)hipErrorOutOfMemory;
-    SegTask* tasks = (SegTask*)(dw + d_tasks);
-    SegRes* res = (SegRes*)(dw + d_res);
-    uint32_t* fb = (uint32_t*)(dw + d_fb);
-    uint16_t* sym = (uint16_t*)(dw + d_sym);
-    uint32_t* rmap = (uint32_t*)(dw + d_map);
-    uint32_t* marked = (uint32_t*)(dw + d_mark);
-    if (hipMemsetAsync(marked, 0, 4ull * n, s) != hipSuccess) return (int)hipErrorUnknown;
     // scan: one wave per region, SCAN_WAVES waves per workgroup, ~3
     // workgroups per CU by LDS; then the slots, one wave per payload
-    hipLaunchKernelGGL(bp_region_map_kernel, dim3((n + 255) / 256), dim3(256), 0, s, nlong, reg, tbase, rmap);
+    hipLaunchKernelGGL(bp_region_map_kernel, dim3((n + 255) / 256), dim3(256), 0, s, fit, reg, tbase, rmap);
     const uint32_t scan_wgs = 3u * cus;
     hipLaunchKernelGGL(bp_scan_kernel<false>, dim3(scan_wgs), dim3(64 * SCAN_WAVES), 0, s, in, in_off, in_len, order,
-                       rmap, (uint32_t)ntask, st, tbase, tasks, marked);
+                       rmap, fit + 1, st, tbase, tasks, marked);
     hipLaunchKernelGGL(bp_scan_kernel<true>, dim3(scan_wgs), dim3(64 * SCAN_WAVES), 0, s, in, in_off, in_len, order,
-                       rmap, (uint32_t)ntask, st, tbase, tasks, marked);
-    hipLaunchKernelGGL(bp_slots_kernel, dim3(4u * cus), dim3(256), 0, s, in_len, order, nlong, st, tbase,
+                       rmap, fit + 1, st, tbase, tasks, marked);
+    hipLaunchKernelGGL(bp_slots_kernel, dim3(4u * cus), dim3(256), 0, s, in_len, order, fit, st, tbase,
                        wbase, tasks);
     if (hipGetLastError() != hipSuccess) return (int)hipErrorUnknown;
+    // segments: a work queue over the device-side task count
     const uint32_t wgs = 4u * cus;
-    int e = bpmd_internal_inflate_lane3_seg(in, in_off, in_len, (uint32_t)ntask, tasks, sym, res, raw,
-                                            (uint64_t)ntask > (uint64_t)wgs * 64u ? q + 3 : nullptr, wgs, s);
+    int e = bpmd_internal_inflate_lane3_seg(in, in_off, in_len, (uint32_t)cap_tasks, tasks, sym, res, raw, q + 3, wgs,
+                                            s, fit + 1);
     if (e) return e;
-    hipLaunchKernelGGL(bp_resolve_kernel, dim3(8u * cus), dim3(256), 0, s, order, nlong, tbase, tasks, res,
+    hipLaunchKernelGGL(bp_resolve_kernel, dim3(8u * cus), dim3(256), 0, s, order, fit, tbase, tasks, res,
                        sym, out, out_off, out_cap, out_len, status, raw, fb, q + 2, q + 1, st);
     if (hipGetLastError() != hipSuccess) return (int)hipErrorUnknown;
-    // payloads whose output outgrew the slots: the wave kernel, from the list
+    // payloads over the capacity or whose output outgrew the slots: the wave
+    // kernel, from the list
     return bpmd_internal_inflate_wave_ordered(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, raw,
                                               nullptr, fb, q + 2, s);
-}
-
-
-extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n,
-                                        uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
-                                        uint32_t* out_len, int32_t* status, uint32_t raw, const uint32_t* order,
-                                        const uint32_t* nlong, hipStream_t s)
-{
-    uint64_t ntask = 0;
-    const int e = bpmd_internal_inflate_bp_plan(in_len, n, out_cap, order, nlong, s, &ntask);
-    if (e || ntask == 0) return e;
-    return bpmd_internal_inflate_bp_run(in, in_off, in_len, out, out_off, out_cap, out_len, status, raw, order, nlong,
-                                        s);
 }
 
 extern "C" int bpmd_diag_bp_fallback(uint32_t* out8)

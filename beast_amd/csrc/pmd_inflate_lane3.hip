@@ -1514,8 +1514,11 @@ __global__ void __launch_bounds__(128, 2)
 inflate_lane3_seg_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                          const uint32_t* __restrict__ in_len, uint32_t n_tasks, const bp::SegTask* __restrict__ tasks,
                          uint16_t* __restrict__ sym, bp::SegRes* __restrict__ res, uint32_t raw,
-                         uint32_t* __restrict__ qctr)
+                         uint32_t* __restrict__ qctr, const uint32_t* __restrict__ n_dev)
 {
+    // n_dev: the device-side task count (the block-parallel driver sizes
+    // nothing on the host); n_tasks bounds it
+    if (n_dev && *n_dev < n_tasks) n_tasks = *n_dev;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const unsigned lane = threadIdx.x & 63u;
     const bool is_decoder = threadIdx.x < 64;
@@ -1538,14 +1541,15 @@ inflate_lane3_seg_kernel(const uint8_t* __restrict__ in, const uint64_t* __restr
 
 extern "C" int bpmd_internal_inflate_lane3_seg(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                                uint32_t n_tasks, const void* tasks, uint16_t* sym, void* res,
-                                               uint32_t raw, uint32_t* qctr, uint32_t grid_wgs, hipStream_t stream)
+                                               uint32_t raw, uint32_t* qctr, uint32_t grid_wgs, hipStream_t stream,
+                                               const uint32_t* n_dev)
 {
     using namespace bpmd::lp3;
     if (n_tasks == 0) return 0;
     unsigned grid = (n_tasks + WG_MSGS - 1) / WG_MSGS;
     if (qctr && grid_wgs && grid > grid_wgs) grid = grid_wgs;
     hipLaunchKernelGGL(inflate_lane3_seg_kernel, dim3(grid), dim3(128), WG_MSGS * STRIDE, stream, in, in_off, in_len,
-                       n_tasks, (const bpmd::bp::SegTask*)tasks, sym, (bpmd::bp::SegRes*)res, raw, qctr);
+                       n_tasks, (const bpmd::bp::SegTask*)tasks, sym, (bpmd::bp::SegRes*)res, raw, qctr, n_dev);
     return (int)hipGetLastError();
 }
 

@@ -16,10 +16,21 @@
  * Beast's zlib::error values (include/boost/beast/zlib/error.hpp:48-138) in
  * the status array.  Device pointers refer to memory of the current HIP
  * device; `stream` is a hipStream_t (0 = default stream).  Batch calls are
- * asynchronous on `stream`; a call that needs device workspace (work queues,
- * chunk scratch) takes it from a per-stream pool that the first such call on
- * the stream allocates and a larger batch grows.  Concurrent calls from
- * several host threads on one stream are serialised per stream.
+ * asynchronous on `stream`: they enqueue their kernels and return without
+ * waiting for the device (bpmd_inflate_batch / bpmd_read_batch of every size,
+ * the block-parallel path of long payloads included; deflate of messages of
+ * at most 4 KiB), with two exceptions, both waits on `stream`:
+ *   - bpmd_deflate_batch / bpmd_write_batch with a message longer than
+ *     4 KiB (or any context-takeover deflate) read back a 4-byte chunk count
+ *     that sizes their chunk workspace, so they return only once the work
+ *     queued on `stream` before them has run (the short messages' kernel is
+ *     enqueued before the wait and runs meanwhile);
+ *   - a call that needs more device workspace than its stream's pool holds
+ *     (work queues, chunk scratch, block-parallel decode workspace) grows
+ *     the pool, and freeing the smaller block waits for `stream` to drain;
+ *     a stream that repeats one batch shape grows it only on the first calls.
+ * Concurrent calls from several host threads on one stream are serialised
+ * per stream.
  */
 #ifndef BEAST_PMD_H
 #define BEAST_PMD_H

@@ -3,7 +3,7 @@
 cd $GRAFT_REPO_ROOT
 for v in $VARIANTS default; do
   if [ "$v" = default ]; then L=beast_amd/libbeast_pmd.so; else L=beast_amd/libbeast_pmd_$v.so; fi
-  echo "== $v"
-  BPMD_LIB=$L timeout -k 10 200 python bench.py --steps 10 --warmup 2 --no-cpu-baseline ${AB_ARGS} 2>/dev/null \
-    | python -c "import json,sys; d=json.loads(sys.stdin.read()); x=d.get('deflate',{}); print('inflate', d['value'], d['roofline']['kernel_ms'], d['parity_ok'], '| deflate', x.get('deflate_value'), x.get('roundtrip_ok'))" || exit 1
+  BPMD_LIB=$L bash scripts/run_bench.sh ab_$v 200 \
+    "'inflate', d['value'], d['roofline']['kernel_ms'], d['parity_ok'], '| deflate', d.get('deflate',{}).get('deflate_value'), d.get('deflate',{}).get('roundtrip_ok')" \
+    --steps 10 --warmup 2 --no-cpu-baseline ${AB_ARGS} || exit 1
 done

@@ -3,7 +3,7 @@ cd $GRAFT_REPO_ROOT
 for r in $(seq ${ROUNDS:-2}); do
   for v in default $VARIANTS; do
     if [ "$v" = default ]; then L=beast_amd/libbeast_pmd.so; else L=beast_amd/libbeast_pmd_$v.so; fi
-    BPMD_LIB=$L timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-deflate --no-mixed --no-frame 2>/dev/null \
-      | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$v', d['value'], d['roofline']['kernel_ms'], d['parity_ok'])" || exit 1
+    BPMD_LIB=$L bash scripts/run_bench.sh abi_${v}_$r 200 "'$v', d['value'], d['roofline']['kernel_ms'], d['parity_ok']" \
+      --steps 20 --warmup 3 --no-cpu-baseline --no-deflate --no-mixed --no-frame || exit 1
   done
 done

@@ -1,0 +1,86 @@
+"""Which batch calls return before the device has run the work queued ahead
+of them (include/beast_pmd.h, "Batch calls are asynchronous on stream").
+
+A long device copy is queued on the caller's stream first; a call that does
+not wait on the device returns while that copy is still running (the stream
+is not idle and the call took a small part of the copy's time).  The
+block-parallel inflate path sizes its workspace without a read-back, so
+bpmd_inflate_batch returns at once even on a batch of long payloads;
+bpmd_deflate_batch with a message over 4 KiB reads back its chunk count and
+returns only after the copy, as the header states."""
+import time
+
+import numpy as np
+import pytest
+
+from beast_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup():
+    import torch
+    from beast_amd import pmd
+    dev = torch.device("cuda", 0)
+    big = torch.empty(3 << 30, dtype=torch.uint8, device=dev)
+    big2 = torch.empty_like(big)
+    big2.copy_(big)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    big2.copy_(big)
+    torch.cuda.synchronize()
+    return torch, pmd, dev, big, big2, time.perf_counter() - t0
+
+
+def _timed_call(torch, fn, big, big2):
+    """(host seconds of fn with a copy queued ahead, stream idle right after fn)"""
+    torch.cuda.synchronize()
+    big2.copy_(big)
+    t0 = time.perf_counter()
+    fn()
+    dt = time.perf_counter() - t0
+    idle = torch.cuda.current_stream().query()
+    torch.cuda.synchronize()
+    return dt, idle
+
+
+def test_inflate_block_parallel_batch_does_not_wait():
+    torch, pmd, dev, big, big2, t_copy = _setup()
+    # C5-shaped long payloads in a 2 048-message batch: the block-parallel path
+    raw, off, ln = synth.make_batch("binary", np.full(2048, 65536, np.uint32), seed=0x5EED0055)
+    src = pmd.Batch.from_arrays(raw, off.astype(np.int64), ln.astype(np.int32))
+    d = pmd.deflate_batch(src, level=1)
+    comp = pmd.Batch(d.out.data, d.out.off, d.out.len)
+    cap = torch.from_numpy(ln.astype(np.int32)).to(dev)
+    out = torch.empty_like(src.data)
+
+    def call():
+        return pmd.inflate_batch(comp, cap, out=out, out_off=src.off)
+
+    for _ in range(3):   # the stream's pools reach this batch's size
+        r = call()
+    torch.cuda.synchronize()
+    assert int((r.status != 0).sum()) == 0 and torch.equal(out, src.data)
+    dt, idle = _timed_call(torch, call, big, big2)
+    assert not idle, "the queued copy had finished"
+    assert dt < 0.5 * t_copy, (dt, t_copy)
+
+
+def test_deflate_of_long_messages_waits_for_its_chunk_count():
+    torch, pmd, dev, big, big2, t_copy = _setup()
+    raw, off, ln = synth.make_batch("json", np.full(512, 65536, np.uint32), seed=0x5EED0056)
+    src = pmd.Batch.from_arrays(raw, off.astype(np.int64), ln.astype(np.int32))
+    ub = np.array([pmd.upper_bound(int(x)) for x in ln], dtype=np.int32)
+    cap = torch.from_numpy(ub).to(dev)
+    coff = pmd.slot_offsets(cap)
+    cbuf = torch.empty(int(coff[-1]) + int(ub[-1]) + 64, dtype=torch.uint8, device=dev)
+
+    def call():   # every buffer given: the wrapper itself never waits
+        return pmd.deflate_batch(src, level=6, out_cap=cap, out=cbuf, out_off=coff)
+
+    for _ in range(2):
+        d = call()
+    torch.cuda.synchronize()
+    assert int((d.status != 0).sum()) == 0
+    dt, _ = _timed_call(torch, call, big, big2)
+    assert dt > 0.5 * t_copy, (dt, t_copy)   # documented: it waits for the work queued before it

@@ -185,3 +185,34 @@ def test_final_stored_block_keeps_end_of_stream(mode, raw):
         payloads.append(c.compress(data) + c.flush(zlib.Z_FINISH))
         caps.append(size + 16)
     _check(payloads, caps, raw=raw)
+
+
+@pytest.mark.parametrize("level", [1, 6])
+def test_c5_payload_with_false_stored_candidate(level):
+    """The bench's C5 message 11145 (seed 0x5EED0005), as this library
+    deflates it, holds a random LEN / NLEN pair at byte 53 863 whose LEN
+    (6 857) lands exactly on a real block start, so the stored-block check
+    passes it.  With slots sized to the next candidate only, the real segment
+    before it outgrew its slot and the payload fell back to the wave kernel
+    (f59740b: slots reach to the candidate after next).  Forced block-parallel,
+    the payload must decode exactly and without a fallback."""
+    import ctypes
+    import torch
+    pmd = _pmd()
+    raw, off, ln = synth.make_batch("binary", np.full(1, 65536, np.uint32), seed=0x5EED0005, first=11145)
+    src = pmd.Batch.from_arrays(raw, off.astype(np.int64), ln.astype(np.int32))
+    d = pmd.deflate_batch(src, level=level, mem_level=4)
+    torch.cuda.synchronize()
+    assert int(d.status[0]) == 0
+    c = (ctypes.c_ulonglong * 12)()
+    pmd.lib().bpmd_diag_bp_counters(c, 1)
+    assert pmd.lib().bpmd_set_inflate_kernel(3) == 0
+    try:
+        r = pmd.inflate_batch(pmd.Batch(d.out.data, d.out.off, d.out.len), torch.tensor([65536], dtype=torch.int32))
+        torch.cuda.synchronize()
+    finally:
+        pmd.lib().bpmd_set_inflate_kernel(0)
+    pmd.lib().bpmd_diag_bp_counters(c, 1)
+    assert int(r.status[0]) == 0 and int(r.out.len[0]) == 65536
+    assert torch.equal(r.out.data[:65536], src.data[:65536])
+    assert c[0] == 1 and c[1] >= 8 and c[2] == 0, list(c)[:3]   # one payload, its segments, no fallback
