@@ -69,7 +69,7 @@ extern "C" int bpmd_internal_slide(uint8_t* buf, const uint64_t* base, const uin
 
 namespace {
 std::mutex g_init_mu;
-int g_init_device = -1;   // device whose symbols are initialised
+uint64_t g_init_devices = 0;   // bit d: device d's symbols are initialised
 
 // Per (device, stream) scratch for batch calls that need device workspace
 // (work-queue counters, message order, chunk workspace).  Allocated on first
@@ -230,6 +230,10 @@ extern "C" void bpmd_internal_scratch_release(hipStream_t s)
     }
 }
 
+// the launch lock of a stream (pmd_multi.hip takes it around its own
+// scratch use, as scratch_for requires)
+extern "C" void* bpmd_internal_stream_mutex(hipStream_t s) { return stream_mutex(s); }
+
 // Number of scratch blocks held (footprint tests)
 extern "C" size_t bpmd_internal_scratch_count(void)
 {
@@ -299,9 +303,10 @@ extern "C" int bpmd_init(void)
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return BPMD_R_NO_DEVICE;
     std::lock_guard<std::mutex> lk(g_init_mu);
-    if (g_init_device == dev) return BPMD_R_OK;
+    const uint64_t bit = dev < 64 ? 1ull << dev : 0ull;
+    if (g_init_devices & bit) return BPMD_R_OK;
     if (bpmd_internal_init_fixed() != 0) return BPMD_R_HIP_ERROR;
-    g_init_device = dev;
+    g_init_devices |= bit;
     return BPMD_R_OK;
 }
 

@@ -15,6 +15,7 @@
 // all-gather instead (beast_amd/shard.py global_output_offsets).
 #include <hip/hip_runtime.h>
 
+#include <mutex>
 #include <vector>
 
 #include "../../include/beast_pmd.h"
@@ -34,6 +35,8 @@ __global__ void sum_lens_kernel(const uint32_t* __restrict__ len, uint32_t n, un
 
 typedef int (*batch_fn)(const bpmd_cfg*, const uint8_t*, const uint64_t*, const uint32_t*, uint32_t, uint8_t*,
                         const uint64_t*, const uint32_t*, uint32_t*, int32_t*, void*);
+
+extern "C" void* bpmd_internal_stream_mutex(hipStream_t s);
 
 int run_multi(batch_fn fn, const bpmd_cfg* cfg, const bpmd_shard* shards, int n_shards, uint64_t* out_bytes)
 {
@@ -56,7 +59,14 @@ int run_multi(batch_fn fn, const bpmd_cfg* cfg, const bpmd_shard* shards, int n_
                s.d_status, s.stream);
         if (r || !out_bytes) continue;
         const hipStream_t hs = (hipStream_t)s.stream;
-        // per-shard total on the shard's own stream, after its batch (scratch block 8)
+        // per-shard total on the shard's own stream, after its batch (scratch
+        // block 8), under the stream's launch lock like every scratch user
+        std::mutex* mu = (std::mutex*)bpmd_internal_stream_mutex(hs);
+        if (!mu) {
+            r = BPMD_R_HIP_ERROR;
+            break;
+        }
+        std::lock_guard<std::mutex> launch(*mu);
         sums[i] = (unsigned long long*)bpmd_internal_scratch(hs, 256, 8);
         if (!sums[i] || hipMemsetAsync(sums[i], 0, sizeof(unsigned long long), hs) != hipSuccess) {
             r = BPMD_R_HIP_ERROR;
