@@ -97,6 +97,7 @@ struct alignas(16) DefLds {
 
 static_assert(sizeof(DefLds<0>) == 160 * 1024 / 8, "single-chunk deflate LDS: 8 waves per CU");
 static_assert(sizeof(DefLds<2048>) == 26624, "history deflate LDS: 6 waves per CU");
+static_assert(offsetof(DefLds<0>, b) % 16 == 0 && offsetof(DefLds<2048>, b) % 16 == 0, "tok[] is cleared with 16-byte stores");
 static_assert(offsetof(HuffLds, lf) == 0, "bit buffer spill lands in lf[] (dead while packing)");
 
 struct Params {
@@ -261,6 +262,34 @@ __device__ __forceinline__ void for_tokens(const LaneToks& T, const uint16_t* to
             f(true, (e & 0xFFu) + 3, d);
         } else {
             f(false, e, 0u);
+        }
+    }
+}
+
+// for_tokens for the first pass after the parse, whose literal tokens are
+// still zero in tok[]: their bytes come from the window and are stored for
+// the later passes
+template <class F>
+__device__ __forceinline__ void for_tokens_fill(const LaneToks& T, uint16_t* tok, unsigned a0, const Win& W, F f)
+{
+    if (T.rem_kind == 1) f(true, T.rem_len, T.rem_dist);
+    else if (T.rem_kind == 2) {
+        f(false, T.rem_b0, 0u);
+        if (T.rem_len > 1) f(false, T.rem_b1, 0u);
+    }
+    uint64_t m = T.kept;
+    while (m) {
+        const unsigned t = (unsigned)__builtin_ctzll(m);
+        m &= m - 1;
+        const unsigned pos = T.a + t;
+        const uint32_t e = tok[pos - a0];
+        if (e & 0x8000u) {
+            const unsigned d = pos + 1 < T.b ? (unsigned)tok[pos + 1 - a0] + 1 : T.lastdist;
+            f(true, (e & 0xFFu) + 3, d);
+        } else {
+            const uint32_t v = W.byte(pos);
+            tok[pos - a0] = (uint16_t)v;
+            f(false, v, 0u);
         }
     }
 }
@@ -735,24 +764,47 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
         W.ws = load_window(S, msg + wb, wn);
         const bool chains = P.strategy != 2 && P.strategy != 3;
         if (chains) {
-            for (unsigned i = lane; i < HSIZE; i += WAVE) S.b.head[i] = 0xFFFFFFFFu;
+            uint4* h4 = (uint4*)S.b.head;
+            for (unsigned i = lane; i < HSIZE / 4; i += WAVE) h4[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
         }
         wave_sync();
         pf.lap(0);
         // ---- hash chains
         if (chains) {
-            for (unsigned g = 0; g < wn; g += WAVE) {
-                const unsigned q = g + lane;
-                uint32_t pv = NONE;
-                if (q + MIN_MATCH <= wn) {
-                    const uint32_t h = chain_hash(W.dw(q), wn - q, HB);
-                    const uint32_t pre = S.b.head[h];
-                    const uint32_t old = atomicExch(&S.b.head[h], q);
-                    const uint32_t c = old < q ? old : pre;
-                    atomicMax(&S.b.head[h], q);
-                    pv = c < NONE ? c : NONE;
+            // pass 1: every position's hash into prev[] (independent loads);
+            // 0xFFFF = fewer than MIN_MATCH bytes left, not inserted
+            for (unsigned q = lane; q < wn; q += WAVE)
+                S.a.prev[q] = (uint16_t)(q + MIN_MATCH <= wn ? chain_hash(W.dw(q), wn - q, HB) : 0xFFFFu);
+            wave_sync();
+            // pass 2: 64 positions per step, four steps' LDS operations issued
+            // together (a wave's LDS operations run in issue order, so step
+            // j + 1 still sees step j's head updates): link each position to
+            // the head of its hash (or to a lower lane of the same step that
+            // exchanged first), then raise the head to the step's highest
+            constexpr unsigned U = 4;
+            for (unsigned g = 0; g < wn; g += U * WAVE) {
+                uint32_t h[U], pre[U], old[U];
+#pragma unroll
+                for (unsigned j = 0; j < U; ++j) {
+                    const unsigned q = g + j * WAVE + lane;
+                    h[j] = q < wn ? (uint32_t)S.a.prev[q] : 0xFFFFu;
                 }
-                if (q < wn) S.a.prev[q] = (uint16_t)pv;
+#pragma unroll
+                for (unsigned j = 0; j < U; ++j) {
+                    const unsigned q = g + j * WAVE + lane;
+                    pre[j] = old[j] = NONE;
+                    if (h[j] != 0xFFFFu) {
+                        pre[j] = S.b.head[h[j]];
+                        old[j] = atomicExch(&S.b.head[h[j]], q);
+                        atomicMax(&S.b.head[h[j]], q);
+                    }
+                }
+#pragma unroll
+                for (unsigned j = 0; j < U; ++j) {
+                    const unsigned q = g + j * WAVE + lane;
+                    const uint32_t c = old[j] < q ? old[j] : pre[j];
+                    if (q < wn) S.a.prev[q] = (uint16_t)(c < NONE ? c : NONE);
+                }
             }
         }
         wave_sync();
@@ -766,6 +818,108 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
         const bool active = a < wn;
         uint64_t bm = 0;
         unsigned own_end = 0, lastdist = 0;
+#ifndef BPMD_PARSE1
+        // literal tokens are not written by the parse (the histogram pass
+        // takes them from the window): tok[] starts zeroed, matches set 0x8000
+        {
+            uint4* t4 = (uint4*)S.b.tok;
+            for (unsigned i = lane; i < CHUNK * 2 / 16; i += WAVE) t4[i] = make_uint4(0, 0, 0, 0);
+        }
+        wave_sync();
+        if (active) {
+            // The reference's parse loop (f_fast / f_slow) and longest_match
+            // chain walk, flattened into one state machine so that every
+            // iteration does one unit of work per lane (one chain candidate,
+            // or 8 more bytes of a match) -- nested divergent loops would
+            // multiply lane imbalance.  A find's setup (chain head, limits)
+            // runs at the end of the iteration that finished the previous
+            // find, so a find costs no iteration of its own.
+            // The level's limits are wave-uniform, but kept in VGPRs here: in
+            // scalar registers the loop's many lane masks push them out to
+            // VGPR lanes, reloaded (v_readlane) every iteration.
+            const unsigned max_dist = to_vgpr(P.max_dist), good = to_vgpr(P.L.good), nice_l = to_vgpr(P.L.nice),
+                           lazy_l = to_vgpr(P.L.lazy), chain_max = to_vgpr(P.chain);
+            const unsigned pflags = to_vgpr((P.L.parser == P_SLOW ? 1u : 0u) | (P.strategy == 2 ? 2u : 0u) |
+                                            (P.strategy == 3 ? 4u : 0u) | (P.strategy == 1 ? 8u : 0u));
+            const bool lazy = (pflags & 1u) != 0, no_match = (pflags & 2u) != 0, rle = (pflags & 4u) != 0,
+                       filtered = (pflags & 8u) != 0;
+            unsigned p = a, l0 = 0, d0 = 0;
+            bool have0 = false;
+            bool mt = false;   // match state (chain otherwise)
+            unsigned q = p, thr = MIN_MATCH - 1, c = 0, chain_left = 0, best = thr, bd = 0, nice = 0, maxl = 0,
+                     l = 0;
+            // find setup at q: chain head and limits; no candidate (c = NONE)
+            // ends the find at the next iteration with best = thr
+            auto setup = [&]() {
+                maxl = wn - q < (unsigned)MAX_MATCH ? wn - q : (unsigned)MAX_MATCH;
+                uint32_t h = S.a.prev[q];
+                asm volatile("" : "+v"(h));   // one load for every lane, not a branch on rle
+                c = rle ? (q > 0 ? q - 1 : NONE) : h;
+                c = (no_match || q + MIN_MATCH > wn) ? NONE : c;
+                chain_left = rle ? 1u : (thr >= good ? chain_max >> 2 : chain_max);
+                nice = rle ? maxl : (nice_l < maxl ? nice_l : maxl);
+            };
+            setup();
+            while (p < b) {
+                ++iters;
+                // every load issued up front
+                const unsigned cc = c < wn ? c : 0;
+                const uint32_t pn = S.a.prev[cc];
+                const uint32_t cb = W.byte(cc + best), qb = W.byte(q + best);
+                const uint64_t cv = W.qw(cc + l), qv = W.qw(q + l);
+                const unsigned k = eq_bytes(cv, qv);
+                const bool ch = !mt;
+                // bitwise, not short-circuit: no branches
+                const bool term = ch & ((c == NONE) | (q - c > max_dist) | (chain_left == 0));
+                const bool test = ch & !term;
+                const bool quick = test & (best < maxl) & (cb == qb) & (k > 0);
+                const bool go_match = quick & (k == 8) & (maxl > 8);
+                const bool ext = mt & (k == 8) & (l + 8 < maxl);
+                const bool have_len = (quick & !go_match) | (mt & !ext);
+                const unsigned len = l + k < maxl ? l + k : maxl;
+                const bool improve = have_len & (len > best);
+                best = improve ? len : best;
+                bd = improve ? q - c : bd;
+                const bool found = term | (improve & (len >= nice));
+                steps += test;
+                chain_left -= test;
+                const bool advance = !found & ((test & !go_match) | (mt & !ext));
+                l = go_match ? 8u : ext ? l + 8 : 0u;
+                c = advance ? pn : c;
+                mt = go_match || ext;
+                if (found) {
+                    // f_slow / f_fast decision, as selects
+                    const bool drop = best > thr && best <= 5 &&
+                                      (filtered || (best == (unsigned)MIN_MATCH && bd > (unsigned)TOO_FAR));
+                    const unsigned lr = drop ? thr : best;
+                    const bool lit = have0 ? lr > l0 : lr < (unsigned)MIN_MATCH;
+                    const bool emit1 = have0 && lr <= l0;          // the pending match wins
+                    const bool take = have0 ? lr > l0 : lr >= (unsigned)MIN_MATCH;   // (lr, bd) pending
+                    unsigned el = l0, ed = d0;
+                    l0 = take ? lr : l0;
+                    d0 = take ? bd : d0;
+                    bm |= (uint64_t)lit << (p - a);
+                    p += lit;
+                    const bool emit2 = !emit1 && take && p < b && !(lazy && l0 < lazy_l && p + 1 < wn);
+                    el = emit1 ? el : l0;
+                    ed = emit1 ? ed : d0;
+                    have0 = take && !emit2;
+                    if (emit1 || emit2) {
+                        S.b.tok[p - a0] = (uint16_t)(0x8000u | (el - MIN_MATCH));
+                        if (p + 1 < b) S.b.tok[p + 1 - a0] = (uint16_t)(ed - 1);
+                        else lastdist = ed;
+                        bm |= 1ull << (p - a);
+                        p += el;
+                    }
+                    q = have0 ? p + 1 : p;
+                    thr = have0 ? l0 : (unsigned)(MIN_MATCH - 1);
+                    best = thr;
+                    bd = 0;
+                    ++finds;
+                    setup();
+                }
+            }
+#else
         if (active) {
             // The reference's parse loop (f_fast / f_slow) and longest_match
             // chain walk, flattened into one state machine so that every
@@ -878,6 +1032,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
                     ++finds;
                 }
             }
+#endif
             own_end = p;
         }
         wave_sync();
@@ -888,6 +1043,8 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
         pf.cnt(21, wave_sum(finds));
         pf.cnt(18, 1);
         pf.cnt(22, wave_maxu(iters));
+        pf.cnt(23, wave_sum(iters));
+        pf.cnt(16, wave_sum(active ? 1u : 0u));
 #endif
         // ---- boundary repair
         const unsigned E = wave_scan_max_excl(own_end, a0);
@@ -925,7 +1082,11 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
             else H.bf[i - 320] = 0;
         }
         wave_sync();
+#ifndef BPMD_PARSE1
+        for_tokens_fill(T, S.b.tok, a0, W, [&](bool is_match, unsigned v, unsigned dist) {
+#else
         for_tokens(T, S.b.tok, a0, [&](bool is_match, unsigned v, unsigned dist) {
+#endif
             ++n_tok;
             if (!is_match) { atomicAdd(&H.lf[v], 1u); return; }
             ++n_match;

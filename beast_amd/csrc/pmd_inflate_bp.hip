@@ -91,9 +91,11 @@ bp_sum_kernel(const uint32_t* __restrict__ in_len, const uint32_t* __restrict__ 
     if ((threadIdx.x & 63) == 0 && acc) atomicAdd(total, acc);
 }
 
-// Region size: about SEG_OUT of output at the payload's provisioned ratio,
-// but no smaller than the batch's long bytes over 2 segments per lane of
-// the chip (more segments only cost scanning once every lane has two).
+// Region size: the batch's long bytes over 2 segments per lane of the chip
+// (more segments only cost scanning once every lane has two), within
+// [R_MIN, R_MAX].  Round 3 never went below SEG_OUT of output at the
+// payload's provisioned ratio (-DBPMD_BP_R_FLOOR), which left an 8-way shard
+// of C5 with 4 KiB regions and half the chip's lanes idle.
 __global__ void __launch_bounds__(256)
 bp_stats_kernel(const uint32_t* __restrict__ in_len, const uint32_t* __restrict__ out_cap,
                 const uint32_t* __restrict__ order, const uint32_t* __restrict__ nlong, uint32_t n,
@@ -112,7 +114,16 @@ bp_stats_kernel(const uint32_t* __restrict__ in_len, const uint32_t* __restrict_
         const uint64_t e16 = cap >= 4ull * len ? (4ull << 16) : (((uint64_t)cap << 16) / (len ? len : 1u));
         uint64_t R = cap ? ((uint64_t)SEG_OUT * len) / cap : R_MAX;
         const uint64_t share = *total / ((uint64_t)segs_per_lane * (lanes ? lanes : 1u));
+#ifdef BPMD_BP_R_FLOOR   // diagnostics: round 3's rule (never below SEG_OUT of output)
         R = R < share ? share : R;
+#else
+        // the share alone: a batch with fewer long bytes than the chip's lanes
+        // want cuts its payloads finer, down to R_MIN (about one of Beast's
+        // 1023-symbol blocks of near-random data; an 8-way shard of C5 has
+        // 1 KiB a lane), not at SEG_OUT of output
+        (void)R;
+        R = share;
+#endif
         R = R < R_MIN ? R_MIN : R > R_MAX ? R_MAX : R;
         R &= ~255ull;
         na = (uint32_t)((len + R / 2) / R);   // a last region shorter than R / 2 joins the one before

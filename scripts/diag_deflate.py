@@ -19,7 +19,8 @@ NAMES = {0: "window+head init", 1: "hash chains", 2: "parse", 3: "repair+histogr
          5: "merge (serial)", 6: "depths", 7: "limit+scatter", 8: "canonical codes", 9: "rle+bl tree (lane0)",
          10: "costs", 11: "stored emit", 12: "token bit count", 13: "zero+header (lane0)", 14: "token emit",
          15: "global copy", 18: "#chunks", 19: "chain steps (sum lanes)", 20: "chain steps (max lane)",
-         21: "find calls (sum lanes)", 22: "parse iterations (max lane)"}
+         21: "find calls (sum lanes)", 22: "parse iterations (max lane)",
+         23: "parse iterations (sum lanes)", 16: "active parse lanes"}
 
 
 def main():
