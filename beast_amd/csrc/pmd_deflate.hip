@@ -465,6 +465,49 @@ __device__ void bl_tree_wave(HuffLds& H, uint32_t& hdr_bits, uint32_t& nbl_out)
 
 // Lit/len and distance code lengths + canonical codes for the current
 // histograms (H.lf with EOB counted, H.df).  Whole wave.
+// Bitonic sort (ascending) of the 64 * R keys at k[0, 64 R), element
+// lane * R + r in register r of its lane: partners less than R apart are
+// compare-exchanged in registers, the others across lanes by xor shuffles.
+template <int R>
+__device__ __forceinline__ void sort_keys_reg(uint32_t* keys)
+{
+    const unsigned lane = lane_id();
+    uint32_t v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = keys[lane * R + r];
+#pragma unroll
+    for (unsigned k = 2; k <= 64u * R; k <<= 1) {
+#pragma unroll
+        for (unsigned j = k >> 1; j > 0; j >>= 1) {
+            if (j < (unsigned)R) {
+#pragma unroll
+                for (unsigned r = 0; r < (unsigned)R; ++r) {
+                    if (r & j) continue;
+                    const unsigned e = lane * R + r;
+                    const bool up = (e & k) == 0;
+                    const uint32_t x = v[r], y = v[r ^ j];
+                    const bool sw = (x > y) == up;
+                    v[r] = sw ? y : x;
+                    v[r ^ j] = sw ? x : y;
+                }
+            } else {
+                const unsigned lm = j / R;   // partner lane distance
+                const bool lower = (lane & lm) == 0;
+#pragma unroll
+                for (unsigned r = 0; r < (unsigned)R; ++r) {
+                    const unsigned e = lane * R + r;
+                    const bool up = (e & k) == 0;
+                    const uint32_t y = (uint32_t)__shfl_xor((int)v[r], (int)lm);
+                    const uint32_t mn = v[r] < y ? v[r] : y, mx = v[r] < y ? y : v[r];
+                    v[r] = (lower == up) ? mn : mx;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) keys[lane * R + r] = v[r];
+}
+
 __device__ void build_trees(HuffLds& H, Prof& pf)
 {
     const unsigned lane = lane_id();
@@ -512,6 +555,7 @@ __device__ void build_trees(HuffLds& H, Prof& pf)
         for (unsigned i = at + lane; i < P; i += WAVE) H.keys[i] = 0xFFFFFFFFu;
         wave_sync();
     }
+#ifdef BPMD_SORT_LDS   // diagnostics: round 3's bitonic sort through LDS
     // --- bitonic sort of P keys (P / 128 compare-exchanges per lane per stage)
     for (unsigned k = 2; k <= P; k <<= 1) {
         for (unsigned j = k >> 1; j > 0; j >>= 1) {
@@ -527,6 +571,13 @@ __device__ void build_trees(HuffLds& H, Prof& pf)
             wave_sync();
         }
     }
+#else
+    // --- bitonic sort of P keys in registers (P / 64 per lane)
+    if (P == 128) sort_keys_reg<2>(H.keys);
+    else if (P == 256) sort_keys_reg<4>(H.keys);
+    else sort_keys_reg<8>(H.keys);
+    wave_sync();
+#endif
     pf.lap(4);
     const unsigned ml = used_l, md = used_d;
     // a wide literal/length alphabet takes Shannon lengths (lz_core.h), no merge
