@@ -13,7 +13,7 @@ for cfg in "json 4096 6 65536" "json 65536 6 4096" "binary 65536 1 4096"; do
     timeout -k 10 120 python -u scripts/diag_deflate.py > gpurun_out/diag_$1_$2.log 2>&1 || exit 4
   grep "msgs\|parse\|active\|total" gpurun_out/diag_$1_$2.log
 done
-for v in $BP_VARIANTS; do
+for v in $BP_VARIANTS; do  # (optional)
   for pr in gpu beast; do
     BPMD_LIB=$PWD/beast_amd/$v timeout -k 10 150 python -u scripts/diag_bp.py case binary 2048 65536 $pr 1 auto 2>&1 | grep -v amdgpu.ids || exit 5
   done
