@@ -266,9 +266,9 @@ __device__ __forceinline__ void for_tokens(const LaneToks& T, const uint16_t* to
     }
 }
 
-// for_tokens for the first pass after the parse, whose literal tokens are
-// still zero in tok[]: their bytes come from the window and are stored for
-// the later passes
+// for_tokens for the first pass after the parse, which leaves literal tokens
+// zero in tok[]: their bytes come from the window and are stored for the
+// later passes
 template <class F>
 __device__ __forceinline__ void for_tokens_fill(const LaneToks& T, uint16_t* tok, unsigned a0, const Win& W, F f)
 {
@@ -822,40 +822,24 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
         pf.lap(0);
         // ---- hash chains
         if (chains) {
-            // pass 1: every position's hash into prev[] (independent loads);
-            // 0xFFFF = fewer than MIN_MATCH bytes left, not inserted
-            for (unsigned q = lane; q < wn; q += WAVE)
-                S.a.prev[q] = (uint16_t)(q + MIN_MATCH <= wn ? chain_hash(W.dw(q), wn - q, HB) : 0xFFFFu);
-            wave_sync();
-            // pass 2: 64 positions per step, four steps' LDS operations issued
-            // together (a wave's LDS operations run in issue order, so step
-            // j + 1 still sees step j's head updates): link each position to
-            // the head of its hash (or to a lower lane of the same step that
-            // exchanged first), then raise the head to the step's highest
-            constexpr unsigned U = 4;
-            for (unsigned g = 0; g < wn; g += U * WAVE) {
-                uint32_t h[U], pre[U], old[U];
-#pragma unroll
-                for (unsigned j = 0; j < U; ++j) {
-                    const unsigned q = g + j * WAVE + lane;
-                    h[j] = q < wn ? (uint32_t)S.a.prev[q] : 0xFFFFu;
+            // 64 positions per step: link each position to the head of its
+            // hash (or to a lower lane of the same step that exchanged first),
+            // then raise the head to the step's highest position.  (Measured
+            // and dropped: hashes first into prev[], then four steps' LDS
+            // atomics in flight together -- 573 K -> 653 K cycles per C4
+            // message, profiles/r04x_diag_deflate_phases.log.)
+            for (unsigned g = 0; g < wn; g += WAVE) {
+                const unsigned q = g + lane;
+                uint32_t pv = NONE;
+                if (q + MIN_MATCH <= wn) {
+                    const uint32_t h = chain_hash(W.dw(q), wn - q, HB);
+                    const uint32_t pre = S.b.head[h];
+                    const uint32_t old = atomicExch(&S.b.head[h], q);
+                    const uint32_t c = old < q ? old : pre;
+                    atomicMax(&S.b.head[h], q);
+                    pv = c < NONE ? c : NONE;
                 }
-#pragma unroll
-                for (unsigned j = 0; j < U; ++j) {
-                    const unsigned q = g + j * WAVE + lane;
-                    pre[j] = old[j] = NONE;
-                    if (h[j] != 0xFFFFu) {
-                        pre[j] = S.b.head[h[j]];
-                        old[j] = atomicExch(&S.b.head[h[j]], q);
-                        atomicMax(&S.b.head[h[j]], q);
-                    }
-                }
-#pragma unroll
-                for (unsigned j = 0; j < U; ++j) {
-                    const unsigned q = g + j * WAVE + lane;
-                    const uint32_t c = old[j] < q ? old[j] : pre[j];
-                    if (q < wn) S.a.prev[q] = (uint16_t)(c < NONE ? c : NONE);
-                }
+                if (q < wn) S.a.prev[q] = (uint16_t)pv;
             }
         }
         wave_sync();
@@ -869,9 +853,11 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
         const bool active = a < wn;
         uint64_t bm = 0;
         unsigned own_end = 0, lastdist = 0;
-#ifndef BPMD_PARSE1
         // literal tokens are not written by the parse (the histogram pass
-        // takes them from the window): tok[] starts zeroed, matches set 0x8000
+        // takes them from the window): tok[] starts zeroed, matches set 0x8000.
+        // (Measured and dropped: the literal's byte loaded with every
+        // iteration's other loads and stored by the parse -- C4 26.2 -> 25.2
+        // GiB/s, profiles/r04y_ab_literal_preload_rejected.log.)
         {
             uint4* t4 = (uint4*)S.b.tok;
             for (unsigned i = lane; i < CHUNK * 2 / 16; i += WAVE) t4[i] = make_uint4(0, 0, 0, 0);
@@ -970,120 +956,6 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
                     setup();
                 }
             }
-#else
-        if (active) {
-            // The reference's parse loop (f_fast / f_slow) and longest_match
-            // chain walk, flattened into one state machine so that every
-            // iteration does one unit of work per lane (a parse decision, one
-            // chain candidate, or 8 more bytes of a match) -- nested
-            // divergent loops would multiply lane imbalance.
-            // The level's limits are wave-uniform, but kept in VGPRs here: in
-            // scalar registers the loop's many lane masks push them out to
-            // VGPR lanes, reloaded (v_readlane) every iteration.
-            const unsigned max_dist = to_vgpr(P.max_dist), good = to_vgpr(P.L.good), nice_l = to_vgpr(P.L.nice),
-                           lazy_l = to_vgpr(P.L.lazy), chain_max = to_vgpr(P.chain);
-            const unsigned pflags = to_vgpr((P.L.parser == P_SLOW ? 1u : 0u) | (P.strategy == 2 ? 2u : 0u) |
-                                            (P.strategy == 3 ? 4u : 0u) | (P.strategy == 1 ? 8u : 0u));
-            const bool lazy = (pflags & 1u) != 0, no_match = (pflags & 2u) != 0, rle = (pflags & 4u) != 0,
-                       filtered = (pflags & 8u) != 0;
-            unsigned p = a, l0 = 0, d0 = 0;
-            bool have0 = false;
-            // Each iteration is one predicated step for every lane:
-            //   start  the find at q was just set up: take the chain head
-            //   chain  test candidate c (quick reject on the byte at `best`,
-            //          first 8 bytes compared)
-            //   match  compare 8 more bytes of the match with c
-            // with every load issued up front from mode-independent
-            // addresses.  Only the parse decision after a finished find
-            // branches.
-            bool st = true, mt = false;      // start / match state (chain otherwise)
-            unsigned q = p, thr = MIN_MATCH - 1, c = 0, chain_left = 0, best = thr, bd = 0, nice = 0, maxl = 0,
-                     l = 0;
-            while (p < b) {
-                ++iters;
-                const unsigned cc = c < wn ? c : 0;
-                const uint32_t pn = S.a.prev[st ? q : cc];
-                const uint32_t cb = W.byte(cc + best), qb = W.byte(q + best);
-                const uint64_t cv = W.qw(cc + l), qv = W.qw(q + l);
-                const unsigned k = eq_bytes(cv, qv);
-                const bool ch = !st && !mt;
-                const bool term = ch && (c == NONE || q - c > max_dist || chain_left == 0);
-                const bool test = ch && !term;
-                const bool quick = test && best < maxl && cb == qb && k > 0;
-                const bool go_match = quick && k == 8 && maxl > 8;
-                const bool ext = mt && k == 8 && l + 8 < maxl;
-                const bool have_len = (quick && !go_match) || (mt && !ext);
-                const unsigned len = l + k < maxl ? l + k : maxl;
-                const bool improve = have_len && len > best;
-                if (improve) {
-                    best = len;
-                    bd = q - c;
-                }
-                const bool start_done = st && (no_match || q + MIN_MATCH > wn);
-                const bool found = term || start_done || (improve && len >= nice);
-                steps += test;
-                chain_left -= test;
-                const bool advance = !found && ((test && !go_match) || (mt && !ext));
-                l = go_match ? 8u : ext ? l + 8 : 0u;
-                if (st) {
-                    maxl = wn - q < (unsigned)MAX_MATCH ? wn - q : (unsigned)MAX_MATCH;
-                    c = rle ? (q > 0 ? q - 1 : NONE) : pn;
-                    chain_left = rle ? 1u : (thr >= good ? chain_max >> 2 : chain_max);
-                    nice = rle ? maxl : (nice_l < maxl ? nice_l : maxl);
-                } else if (advance) {
-                    c = pn;
-                }
-                mt = go_match || ext;
-                st = false;
-                if (found) {
-                    unsigned lr = best;
-                    if (best > thr && best <= 5 &&
-                        (filtered || (best == (unsigned)MIN_MATCH && bd > (unsigned)TOO_FAR)))
-                        lr = thr;
-                    // f_slow / f_fast decision
-                    bool lit = false, emit = false;
-                    unsigned el = 0, ed = 0;
-                    if (!have0) {
-                        if (lr < (unsigned)MIN_MATCH) lit = true;
-                        else { l0 = lr; d0 = bd; have0 = true; }
-                    } else if (lr > l0) {
-                        lit = true;
-                        l0 = lr;
-                        d0 = bd;
-                    } else {
-                        emit = true;
-                        el = l0;
-                        ed = d0;
-                        have0 = false;
-                    }
-                    if (lit) {
-                        S.b.tok[p - a0] = (uint16_t)W.byte(p);
-                        bm |= 1ull << (p - a);
-                        ++p;
-                    }
-                    if (!emit && have0 && p < b && !(lazy && l0 < lazy_l && p + 1 < wn)) {
-                        emit = true;
-                        el = l0;
-                        ed = d0;
-                        have0 = false;
-                    }
-                    if (emit) {
-                        S.b.tok[p - a0] = (uint16_t)(0x8000u | (el - MIN_MATCH));
-                        if (p + 1 < b) S.b.tok[p + 1 - a0] = (uint16_t)(ed - 1);
-                        else lastdist = ed;
-                        bm |= 1ull << (p - a);
-                        p += el;
-                    }
-                    q = have0 ? p + 1 : p;
-                    thr = have0 ? l0 : (unsigned)(MIN_MATCH - 1);
-                    best = thr;
-                    bd = 0;
-                    st = true;
-                    mt = false;
-                    ++finds;
-                }
-            }
-#endif
             own_end = p;
         }
         wave_sync();
@@ -1133,11 +1005,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
             else H.bf[i - 320] = 0;
         }
         wave_sync();
-#ifndef BPMD_PARSE1
         for_tokens_fill(T, S.b.tok, a0, W, [&](bool is_match, unsigned v, unsigned dist) {
-#else
-        for_tokens(T, S.b.tok, a0, [&](bool is_match, unsigned v, unsigned dist) {
-#endif
             ++n_tok;
             if (!is_match) { atomicAdd(&H.lf[v], 1u); return; }
             ++n_match;
