@@ -433,11 +433,13 @@ __device__ __forceinline__ void expander_seg(uint8_t* T, bool valid, uint32_t m,
         c_src[j] = 0;
         c_w0[j] = c_w1[j] = make_uint4(0, 0, 0, 0);
     }
+    L3_DECL;
     for (;;) {
         bool pending = false;
 #pragma unroll
         for (int j = 0; j < KX; ++j) pending = pending || l_n[j] != 0 || c_kind[j] != 0;
         if (!__ballot(!exited || crem != 0 || srem != 0 || pending)) break;
+        L3_CNT(1);
         bool worked = pending;
         // ================================================ stores, output order
 #pragma unroll
@@ -623,8 +625,12 @@ __device__ __forceinline__ void expander_seg(uint8_t* T, bool valid, uint32_t m,
             }
             if (!exited || k) lds_store(T + O_TAIL, tail);
         }
-        if (!__ballot(worked)) __builtin_amdgcn_s_sleep(BPMD3_ESLEEP);
+        if (!__ballot(worked)) {
+            L3_CNT(2);
+            __builtin_amdgcn_s_sleep(BPMD3_ESLEEP);
+        }
     }
+    L3_FLUSH(4);
 }
 
 // ------------------------------------------------------------------- decoder

@@ -15,7 +15,9 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 from beast_amd import pmd, shard, synth  # noqa: E402
 
-NAMES = ["dec cycles", "dec iters", "dec sleeps", "dec hdr iters", "exp cycles", "exp iters", "exp sleeps"]
+NAMES = ["dec cycles", "dec iters", "dec sleeps", "dec hdr iters", "exp cycles", "exp iters", "exp sleeps",
+         "lanes: header, ring not empty", "dec lap: input+tail", "dec lap: S_DATA", "dec lap: headers",
+         "dec lap: publish+loop", "lanes: data, ring full", "lanes: data, room", "lanes: finished", "lanes: in headers"]
 
 
 def main():
@@ -49,7 +51,9 @@ def main():
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         L.bpmd_diag_lane3_counters(c, 1)
-        print(f"{name}: {dt * 1e3:.2f} ms ok {ok} " + " ".join(f"{NAMES[i]} {c[i]}" for i in range(7)), flush=True)
+        print(f"{name}: {dt * 1e3:.2f} ms ok {ok}", flush=True)
+        for i in range(16):
+            print(f"    {NAMES[i]:32s} {c[i]:16d}", flush=True)
     L.bpmd_set_inflate_kernel(0)
 
 
