@@ -239,8 +239,18 @@ struct LaneToks {
 // kind (a wave then runs one body per token instead of both, which pays off
 // when matches are common); otherwise a literal and a match call site (the
 // wave skips the match body when no lane has a match: binary data).
-template <bool SINGLE = false, class F>
-__device__ __forceinline__ void for_tokens(const LaneToks& T, const uint16_t* tok, unsigned a0, F f)
+// Tokens are taken four at a time, their tok[] entries (and the distance
+// slots after them) loaded together before the bodies run, so a lane waits
+// for one LDS round trip per four tokens instead of one per token.
+// FILL: the first pass after the parse, which leaves literal tokens zero in
+// tok[]: their bytes come from the window and are stored for later passes.
+// G: tokens whose entries are loaded together -- 4 in the single-chunk
+// kernel (C3 deflate +2 %), 1 in the chunk kernel, where the grouped loop
+// cost the parse's register allocation 8 % on C5
+// (profiles/r04zb_ab_token_groups.log)
+template <bool SINGLE = false, bool FILL = false, int G = 1, class F>
+__device__ __forceinline__ void for_tokens(const LaneToks& T, uint16_t* tok, unsigned a0, F f,
+                                           const uint8_t* wb = nullptr)
 {
     if (T.rem_kind == 1) f(true, T.rem_len, T.rem_dist);
     else if (T.rem_kind == 2) {
@@ -249,47 +259,38 @@ __device__ __forceinline__ void for_tokens(const LaneToks& T, const uint16_t* to
     }
     uint64_t m = T.kept;
     while (m) {
-        const unsigned t = (unsigned)__builtin_ctzll(m);
-        m &= m - 1;
-        const unsigned pos = T.a + t;
-        const uint32_t e = tok[pos - a0];
-        const bool mt = (e & 0x8000u) != 0;
-        if (SINGLE) {
-            const unsigned d = (mt && pos + 1 < T.b) ? (unsigned)tok[pos + 1 - a0] + 1 : T.lastdist;
-            f(mt, mt ? (e & 0xFFu) + 3 : e, d);
-        } else if (mt) {
-            const unsigned d = pos + 1 < T.b ? (unsigned)tok[pos + 1 - a0] + 1 : T.lastdist;
-            f(true, (e & 0xFFu) + 3, d);
-        } else {
-            f(false, e, 0u);
+        unsigned pos[G];
+        bool v[G];
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            v[j] = m != 0;
+            pos[j] = T.a + (v[j] ? (unsigned)__builtin_ctzll(m) : 0u);
+            m &= m - 1;
         }
-    }
-}
-
-// for_tokens for the first pass after the parse, which leaves literal tokens
-// zero in tok[]: their bytes come from the window and are stored for the
-// later passes
-template <class F>
-__device__ __forceinline__ void for_tokens_fill(const LaneToks& T, uint16_t* tok, unsigned a0, const Win& W, F f)
-{
-    if (T.rem_kind == 1) f(true, T.rem_len, T.rem_dist);
-    else if (T.rem_kind == 2) {
-        f(false, T.rem_b0, 0u);
-        if (T.rem_len > 1) f(false, T.rem_b1, 0u);
-    }
-    uint64_t m = T.kept;
-    while (m) {
-        const unsigned t = (unsigned)__builtin_ctzll(m);
-        m &= m - 1;
-        const unsigned pos = T.a + t;
-        const uint32_t e = tok[pos - a0];
-        if (e & 0x8000u) {
-            const unsigned d = pos + 1 < T.b ? (unsigned)tok[pos + 1 - a0] + 1 : T.lastdist;
-            f(true, (e & 0xFFu) + 3, d);
-        } else {
-            const uint32_t v = W.byte(pos);
-            tok[pos - a0] = (uint16_t)v;
-            f(false, v, 0u);
+        uint32_t e[G], dn[G], lb[G];
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            e[j] = tok[pos[j] - a0];
+            dn[j] = tok[(pos[j] + 1 < T.b ? pos[j] + 1 : pos[j]) - a0];
+            if (FILL) lb[j] = wb[pos[j]];
+        }
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            if (!v[j]) continue;
+            const bool mt = (e[j] & 0x8000u) != 0;
+            const unsigned d = pos[j] + 1 < T.b ? dn[j] + 1 : T.lastdist;
+            uint32_t lit = e[j];
+            if (FILL && !mt) {
+                lit = lb[j];
+                tok[pos[j] - a0] = (uint16_t)lit;
+            }
+            if (SINGLE) {
+                f(mt, mt ? (e[j] & 0xFFu) + 3 : lit, d);
+            } else if (mt) {
+                f(true, (e[j] & 0xFFu) + 3, d);
+            } else {
+                f(false, lit, 0u);
+            }
         }
     }
 }
@@ -785,6 +786,7 @@ template <int HIST>
 __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base, unsigned len, unsigned hist,
                               const Params& P, MsgOut& o, Prof& pf)
 {
+    constexpr int TOKG = HIST == 0 ? 4 : 1;
     using namespace lz;
     const unsigned lane = lane_id();
     const unsigned cend = base + CHUNK < len ? base + CHUNK : len;
@@ -1005,7 +1007,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
             else H.bf[i - 320] = 0;
         }
         wave_sync();
-        for_tokens_fill(T, S.b.tok, a0, W, [&](bool is_match, unsigned v, unsigned dist) {
+        for_tokens<false, true, TOKG>(T, S.b.tok, a0, [&](bool is_match, unsigned v, unsigned dist) {
             ++n_tok;
             if (!is_match) { atomicAdd(&H.lf[v], 1u); return; }
             ++n_match;
@@ -1014,7 +1016,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
             atomicAdd(&H.lf[s], 1u);
             dist_code(dist, s, nx, xv);
             atomicAdd(&H.df[s], 1u);
-        });
+        }, W.b + W.ws);
         n_tok = wave_sum(n_tok);
         n_match = wave_sum(n_match);
         wave_sync();
@@ -1156,8 +1158,8 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
             nbits += (H.codes[DIST_IDX + s] >> 16) + nx;
         }
     };
-    if (dense) for_tokens<true>(T, S.b.tok, a0, count_bits);
-    else for_tokens<false>(T, S.b.tok, a0, count_bits);
+    if (dense) for_tokens<true, false, TOKG>(T, S.b.tok, a0, count_bits);
+    else for_tokens<false, false, TOKG>(T, S.b.tok, a0, count_bits);
     const uint32_t incl = wave_scan_incl(nbits);
     const uint32_t tok_bits = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     const uint32_t eob_len = H.codes[EOB] >> 16;
@@ -1232,8 +1234,8 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
                 bw.put((c2 & 0xFFFFu) | (xv << (c2 >> 16)), (c2 >> 16) + nx);
             }
         };
-        if (dense) for_tokens<true>(T, S.b.tok, a0, emit);
-        else for_tokens<false>(T, S.b.tok, a0, emit);
+        if (dense) for_tokens<true, false, TOKG>(T, S.b.tok, a0, emit);
+        else for_tokens<false, false, TOKG>(T, S.b.tok, a0, emit);
         bw.flush();
     }
     wave_sync();
