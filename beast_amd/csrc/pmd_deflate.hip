@@ -830,6 +830,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
             // and dropped: hashes first into prev[], then four steps' LDS
             // atomics in flight together -- 573 K -> 653 K cycles per C4
             // message, profiles/r04x_diag_deflate_phases.log.)
+#ifdef BPMD_CHAIN1   // diagnostics: one step at a time
             for (unsigned g = 0; g < wn; g += WAVE) {
                 const unsigned q = g + lane;
                 uint32_t pv = NONE;
@@ -843,6 +844,33 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
                 }
                 if (q < wn) S.a.prev[q] = (uint16_t)pv;
             }
+#else
+            // two steps per iteration: both steps' window loads and hashes
+            // first, then their head operations in step order
+            for (unsigned g = 0; g < wn; g += 2 * WAVE) {
+                const unsigned q0 = g + lane, q1 = q0 + WAVE;
+                const bool i0 = q0 + MIN_MATCH <= wn, i1 = q1 + MIN_MATCH <= wn;
+                const uint32_t w0 = W.dw(i0 ? q0 : 0u), w1 = W.dw(i1 ? q1 : 0u);
+                const uint32_t h0 = chain_hash(w0, wn - q0, HB), h1 = chain_hash(w1, wn - q1, HB);
+                uint32_t pv0 = NONE, pv1 = NONE;
+                if (i0) {
+                    const uint32_t pre = S.b.head[h0];
+                    const uint32_t old = atomicExch(&S.b.head[h0], q0);
+                    const uint32_t c = old < q0 ? old : pre;
+                    atomicMax(&S.b.head[h0], q0);
+                    pv0 = c < NONE ? c : NONE;
+                }
+                if (i1) {
+                    const uint32_t pre = S.b.head[h1];
+                    const uint32_t old = atomicExch(&S.b.head[h1], q1);
+                    const uint32_t c = old < q1 ? old : pre;
+                    atomicMax(&S.b.head[h1], q1);
+                    pv1 = c < NONE ? c : NONE;
+                }
+                if (q0 < wn) S.a.prev[q0] = (uint16_t)pv0;
+                if (q1 < wn) S.a.prev[q1] = (uint16_t)pv1;
+            }
+#endif
         }
         wave_sync();
         pf.lap(1);
