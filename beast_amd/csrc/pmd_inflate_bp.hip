@@ -461,17 +461,26 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
     // static grid stride: regions cost about the same, and one counter
     // taken per region serialises on its atomics (C5: 131 072 regions)
     const uint32_t waves = gridDim.x * SCAN_WAVES;
-    for (uint32_t g = blockIdx.x * SCAN_WAVES + wv; g < n_regions; g += waves) {
-        const uint32_t i = (uint32_t)__builtin_amdgcn_readfirstlane((int)region_map[g]);
-        if (DYN) {
-            // only the regions pass 1 left pending, of unmarked payloads
-            const uint32_t kd = (uint32_t)__builtin_amdgcn_readfirstlane((int)tasks[g].kind);
-            if (kd != KIND_PENDING) continue;
-            if (__builtin_amdgcn_readfirstlane((int)marked[i])) {
-                if (lane == 0) tasks[g].kind = KIND_NONE;
-                continue;
-            }
+    // pass 2 screens 64 regions per step, one per lane (three dependent loads
+    // per region, once per 64 instead of once per region: C4 8-way shard
+    // 0.86 ms of screening), and runs the search on those still to do
+    const uint32_t step = DYN ? 64u : 1u;
+    for (uint32_t g0 = (blockIdx.x * SCAN_WAVES + wv) * step; g0 < n_regions; g0 += waves * step) {
+    uint64_t todo = 1;
+    if (DYN) {
+        // only the regions pass 1 left pending, of unmarked payloads
+        const uint32_t gl = g0 + lane;
+        bool need = false;
+        if (gl < n_regions && tasks[gl].kind == KIND_PENDING) {
+            if (marked[region_map[gl]]) tasks[gl].kind = KIND_NONE;
+            else need = true;
         }
+        todo = __ballot(need);
+    }
+    while (todo) {
+        const uint32_t g = g0 + (uint32_t)__builtin_ctzll(todo);
+        todo &= todo - 1;
+        const uint32_t i = (uint32_t)__builtin_amdgcn_readfirstlane((int)region_map[g]);
         const uint32_t m = order[i];
         const Stat st = stats[i];
         const uint32_t len = in_len[m];
@@ -484,7 +493,12 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
         {
             const uint32_t k = g - tb;
             uint32_t bit = 0, kind = KIND_START;
-            if (k) {
+            // region 0's candidate is the payload's first bit, but pass 1 also
+            // searches it for an empty stored block to mark the payload: a
+            // short payload's only sync marker may lie there, and without the
+            // mark pass 2 would run the bit-offset search on every later region
+            // (C4 8-way shard: 1.06 ms)
+            if (k || !DYN) {
                 kind = KIND_NONE;
                 BP_DIAG(const uint64_t t0 = __builtin_amdgcn_s_memtime());
                 // stage payload bytes from the dword before the region's first
@@ -560,7 +574,10 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
                             atomicAdd(&g_bp_diag[8], t1 - t0);
                             atomicAdd(&g_bp_diag[9], t2 - t1);
                         })
-                if (best != 0xffffffffu) {
+                if (k == 0) {
+                    if (best != 0xffffffffu && best_len == 0 && lane == 0) atomicOr(&marked[i], 1u);
+                    kind = KIND_START;
+                } else if (best != 0xffffffffu) {
                     bit = best;
                     kind = KIND_STORED;
                     if (best_len == 0 && lane == 0) atomicOr(&marked[i], 1u);
@@ -652,6 +669,7 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
             }
         }
         __builtin_amdgcn_wave_barrier();
+    }
     }
 }
 
