@@ -952,13 +952,24 @@ __host__ __device__ constexpr int tier_of(uint32_t len, uint32_t hbits)
     return hbits > 12 ? 2 : len <= Tier<0>::MAX ? 0 : len <= Tier<1>::MAX ? 1 : 2;
 }
 
+// The workspace tier's waves wait on global memory most of the time, so its
+// kernel is held to 4 waves per SIMD (<= 128 VGPRs) for more of them in
+// flight (BPMD_EXACT_T2_OCC; 3 per SIMD unbounded)
+#ifndef BPMD_EXACT_T2_OCC
+#define BPMD_EXACT_T2_OCC 4
+#endif
+#ifndef BPMD_T2_LDS_HEAD
+#define BPMD_T2_LDS_HEAD 2048
+#endif
+constexpr uint32_t T2_LDS_HEAD = BPMD_T2_LDS_HEAD;   // head entries the workspace tier keeps in LDS
 template <int TIER>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64, TIER == 2 ? BPMD_EXACT_T2_OCC : 1)
 deflate_exact_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                      const uint32_t* __restrict__ in_len, uint32_t n, uint8_t* __restrict__ out,
                      const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
                      uint32_t* __restrict__ out_len, int32_t* __restrict__ status, const uint32_t* __restrict__ mask_key,
-                     Cfg c, uint8_t* __restrict__ ws, size_t ws_per_wave)
+                     Cfg c, uint8_t* __restrict__ ws, size_t ws_per_wave, const uint32_t* __restrict__ order,
+                     uint32_t* __restrict__ qctr)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     Trees* T = (Trees*)smem;
@@ -987,11 +998,32 @@ deflate_exact_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict_
         hd = (uint16_t*)p;
         p += 2 * hash_size;
         syms = p;
+        // head[] in LDS beside the trees when it is small (memLevel <= 4:
+        // 4 KiB): one global round trip fewer per inserted position
+        if (hash_size <= T2_LDS_HEAD) hd = (uint16_t*)(smem + ((sizeof(Trees) + 15) & ~(size_t)15));
     }
-    // grid-stride over the messages (the workspace slot is the workgroup's);
-    // each kernel leaves the other's messages
-    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-        const uint32_t len = in_len[i];
+    // the workspace tier takes the messages longest first from a queue (the
+    // order sorts by len >> 6), so the longest start at once and the waves
+    // end together; the LDS tiers stride over the batch.  Each kernel leaves
+    // the other tiers' messages.  (One call site of the message body: two
+    // would inline it twice and double the registers.)
+    uint32_t next = blockIdx.x;
+    for (;;) {
+        uint32_t i, len;
+        if constexpr (TIER == 2) {
+            uint32_t k = 0;
+            if (lane_id() == 0) k = atomicAdd(qctr, 1u);
+            k = U(k);
+            if (k >= n) break;
+            i = U(order[k]);
+            len = U(in_len[i]);
+            if (c.hbits <= 12 && len + 64 <= Tier<1>::MAX) break;   // every later one is shorter
+        } else {
+            if (next >= n) break;
+            i = next;
+            next += gridDim.x;
+            len = in_len[i];
+        }
         if (tier_of(len, c.hbits) != TIER) continue;
         uint8_t* o = out + out_off[i];
         const uint32_t cap = out_cap[i];
@@ -1014,7 +1046,8 @@ deflate_exact_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict_
 }  // namespace bpmd
 
 extern "C" void* bpmd_internal_scratch(hipStream_t s, size_t bytes, int which);
-
+extern "C" const uint32_t* bpmd_internal_lane_order(const uint32_t* in_len, uint32_t n, hipStream_t stream,
+                                                    const uint32_t** keys_out);
 
 // cfg already validated (pmd_capi.hip deflate_impl)
 extern "C" int bpmd_internal_deflate_exact(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
@@ -1039,21 +1072,33 @@ extern "C" int bpmd_internal_deflate_exact(const uint8_t* in, const uint64_t* in
         const size_t tail = 2 * ((size_t)1 << c.hbits) + 3 * (size_t)c.lit_bufsize;
         hipLaunchKernelGGL(deflate_exact_kernel<0>, dim3(n), dim3(64), trees + Tier<0>::WIN + 2 * Tier<0>::PRV + tail,
                            stream, in, in_off, in_len, n, out, out_off, out_cap, out_len, status, mask_key, c,
-                           (uint8_t*)nullptr, (size_t)0);
+                           (uint8_t*)nullptr, (size_t)0, (const uint32_t*)nullptr, (uint32_t*)nullptr);
         if ((e = hipGetLastError()) != hipSuccess) return (int)e;
         hipLaunchKernelGGL(deflate_exact_kernel<1>, dim3(n), dim3(64), trees + Tier<1>::WIN + 2 * Tier<1>::PRV + tail,
                            stream, in, in_off, in_len, n, out, out_off, out_cap, out_len, status, mask_key, c,
-                           (uint8_t*)nullptr, (size_t)0);
+                           (uint8_t*)nullptr, (size_t)0, (const uint32_t*)nullptr, (uint32_t*)nullptr);
         if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     }
-    // the rest: window / prev / head / symbols in a per-wave workspace
+    // the rest: window / prev / head / symbols in a per-wave workspace.  The
+    // waves are latency-bound on it, so as many as the registers allow
+    // (BPMD_EXACT_T2_OCC per SIMD; round 3 ran four per CU), taking the
+    // messages longest first from a queue (BPMD_EXACT_WAVES_PER_CU overrides)
+    static const unsigned wpc = [] {
+        const char* ev = getenv("BPMD_EXACT_WAVES_PER_CU");
+        const unsigned v = ev ? (unsigned)strtoul(ev, nullptr, 10) : 0u;
+        return v ? v : 4u * BPMD_EXACT_T2_OCC;
+    }();
     const size_t wsz = (size_t)1 << c.wbits;
     const size_t per = ((2 * wsz + MAXM + 64 + 15) & ~(size_t)15) + 2 * wsz + 2 * ((size_t)1 << c.hbits) +
                        3 * (size_t)c.lit_bufsize + 64;
-    const unsigned grid = (unsigned)cus * 4u;
+    const unsigned grid = (unsigned)cus * wpc;
     uint8_t* ws = (uint8_t*)bpmd_internal_scratch(stream, per * grid, 4);
-    if (!ws) return (int)hipErrorOutOfMemory;
-    hipLaunchKernelGGL(deflate_exact_kernel<2>, dim3(grid < n ? grid : n), dim3(64), trees, stream, in, in_off,
-                       in_len, n, out, out_off, out_cap, out_len, status, mask_key, c, ws, per);
+    uint32_t* qctr = (uint32_t*)bpmd_internal_scratch(stream, 256, 3);
+    const uint32_t* order = bpmd_internal_lane_order(in_len, n, stream, nullptr);
+    if (!ws || !qctr) return (int)hipErrorOutOfMemory;
+    if (!order || hipMemsetAsync(qctr, 0, sizeof(uint32_t), stream) != hipSuccess) return (int)hipErrorUnknown;
+    const size_t t2_lds = trees + (((size_t)1 << c.hbits) <= T2_LDS_HEAD ? 2 * ((size_t)1 << c.hbits) : 0);
+    hipLaunchKernelGGL(deflate_exact_kernel<2>, dim3(grid < n ? grid : n), dim3(64), t2_lds, stream, in, in_off,
+                       in_len, n, out, out_off, out_cap, out_len, status, mask_key, c, ws, per, order, qctr);
     return (int)hipGetLastError();
 }
