@@ -11,11 +11,12 @@
 // distance codes with an end-of-block code (inflate_stream.ipp:222-354,
 // 574-617).  So:
 //
-//   1. stats (bp_stats_kernel): per long payload a region size R (about 4 KiB
-//      of output per region at the payload's output/input ratio), its region
-//      count and symbol workspace; exclusive sums give every payload's first
-//      task and workspace offset; the totals come back to the host (one
-//      small read-back) to size the workspace;
+//   1. stats (bp_stats_kernel): per long payload a region size R (the
+//      batch's long bytes over two segments per lane of the chip, 1-8 KiB),
+//      its region count and symbol workspace; exclusive sums give every
+//      payload's first task and workspace offset; bp_fit_kernel keeps the
+//      payloads that fit the stream's workspace capacity (the rest go to the
+//      wave kernel) -- no host read-back (see the driver below);
 //   2. scan (bp_scan_kernel, two passes, one wave per region): region 0's
 //      candidate is the payload's first bit; region k > 0 is searched for a
 //      stored block (LEN / NLEN, then a look at the block after it), and a
