@@ -13,21 +13,24 @@
 // exactly this algorithm.
 //
 // Per 4 KiB chunk of a message (small messages: one chunk, no history; large
-// messages: each chunk sees the previous 4 KiB as history):
+// messages: each chunk sees the previous 2 KiB as history, BPMD_CHUNK_HIST):
 //   1. window -> LDS with 16-byte loads;
-//   2. hash chains: 64 positions per step; LDS exchange on a 2^11 head table
-//      links every position to the previous one with the same 3-byte hash;
+//   2. hash chains: 64 positions per step (two steps per iteration); LDS
+//      exchange on a 2^11 head table links every position to the previous
+//      one with the same hash of its next 4 bytes (lz::chain_hash);
 //   3. parse: the chunk is cut into 64 lane segments; each lane runs the
 //      reference's greedy (levels 1-3) or lazy (4-9) matcher with its
 //      chain / lazy / nice / good limits (deflate_stream.hpp:571-590) over
-//      its segment, writing tokens by position and a token-start bitmap;
+//      its segment, writing match tokens by position (literals are taken
+//      from the window afterwards) and a token-start bitmap;
 //   4. boundary repair: an exclusive prefix max of segment end positions
 //      gives each lane the first position it owns; tokens covered by an
 //      earlier lane's last match are dropped and a straddling token keeps
 //      its tail (a match with the same distance, or literals);
-//   5. histograms with LDS atomics, Huffman code lengths (wave bitonic
-//      sort, linear two-queue merge on one lane per tree, depths by pointer
-//      jumping, the reference's 15-bit limit repair), canonical codes;
+//   5. histograms with LDS atomics, Huffman code lengths (bitonic sort of
+//      the used keys in registers, linear two-queue merge on one lane per
+//      tree, depths by pointer jumping, the reference's 15-bit limit
+//      repair; Shannon lengths for wide alphabets), canonical codes;
 //   6. block choice as the reference's tr_flush_block (stored / fixed /
 //      dynamic, deflate_stream.ipp:1425-1518);
 //   7. bit packing: per-lane bit counts, wave prefix sum, ds_or into an LDS
