@@ -12,7 +12,7 @@
 // 574-617).  So:
 //
 //   1. stats (bp_stats_kernel): per long payload a region size R (the
-//      batch's long bytes over two segments per lane of the chip, 1-8 KiB),
+//      batch's long bytes over four segments per lane of the chip, 1-8 KiB),
 //      its region count and symbol workspace; exclusive sums give every
 //      payload's first task and workspace offset; bp_fit_kernel keeps the
 //      payloads that fit the stream's workspace capacity (the rest go to the
@@ -92,8 +92,9 @@ bp_sum_kernel(const uint32_t* __restrict__ in_len, const uint32_t* __restrict__ 
     if ((threadIdx.x & 63) == 0 && acc) atomicAdd(total, acc);
 }
 
-// Region size: the batch's long bytes over 2 segments per lane of the chip
-// (more segments only cost scanning once every lane has two), within
+// Region size: the batch's long bytes over 4 segments per lane of the chip
+// (BPMD_BP_SEGS; finer regions balance the segment kernel's lanes better,
+// at the cost of scanning more regions), within
 // [R_MIN, R_MAX].  Round 3 never went below SEG_OUT of output at the
 // payload's provisioned ratio (-DBPMD_BP_R_FLOOR), which left an 8-way shard
 // of C5 with 4 KiB regions and half the chip's lanes idle.
@@ -1029,7 +1030,7 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
     static const uint32_t segs = [] {
         const char* e = getenv("BPMD_BP_SEGS");
         const uint32_t v = e ? (uint32_t)strtoul(e, nullptr, 10) : 0u;
-        return v ? v : 2u;
+        return v ? v : 4u;   // 2 / 4 / 8: C4 8-way shard 10.3 / 9.1 / 9.3 ms, C5 92 / 96 / 100 GiB/s
     }();
     hipLaunchKernelGGL(bp_stats_kernel, dim3((n + 255) / 256), dim3(256), 0, s, in_len, out_cap, order, nlong, n, total,
                        256u * (uint32_t)cus, segs, st, reg, words);
