@@ -9,6 +9,7 @@ import pytest
 
 from beast_amd import synth
 from oracle import oracle as O
+from tests.foreign import foreign_payloads
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
@@ -154,3 +155,15 @@ def test_full_batch_roundtrip_property():
     got = res.out.data[: n * 4096].view(n, 4096)
     want = torch.from_numpy(data.reshape(n, 4096)).cuda()
     assert torch.equal(got, want)
+
+
+def test_parity_foreign_encoder_flush_mixes():
+    """CPython zlib payloads with mid-payload flushes of every kind, in both
+    framings, at exact, generous and short capacities, against the oracle
+    (the oracle itself is pinned on the same payloads against CPython's
+    inflate in tests/test_oracle_foreign.py)."""
+    pmd_p, raw_p, orig = foreign_payloads(11, 160)
+    rng = random.Random(12)
+    caps = [max(1, rng.choice([len(o), len(o) + 77, len(o) // 2 + 1])) for o in orig]
+    _check_against_oracle(pmd_p, caps)
+    _check_against_oracle(raw_p, caps, raw=True)
