@@ -1,4 +1,5 @@
 # A/B of the side-stream ordering switches on the mixed legs' block-parallel path:
+# (the switches were removed with the rejected change: profiles/r04zzc_bp_lane_wait_prio_rejected.log)
 #   base, BPMD_BP_LANE_WAIT=1, BPMD_BP_SIDE_PRIO=1, both; two rounds interleaved
 cd $GRAFT_REPO_ROOT
 E="{k: (v['inflate_value'], {n: (s.get('inflate_shard_ms'), s['inflate_projected_speedup']) for n, s in v['virtual_shards'].items()}, v['roundtrip_ok']) for k, v in d['mixed'].items() if isinstance(v, dict)}"

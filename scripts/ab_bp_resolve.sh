@@ -1,4 +1,5 @@
 # A/B of the block-parallel resolve with / without loads ahead (BPMD_BP_RESOLVE_PF) on the mixed legs
+# (the switch was removed with the rejected change: profiles/r04zzc_bp_resolve_loads_ahead_rejected.log)
 cd $GRAFT_REPO_ROOT
 E="{k: (v['inflate_value'], {n: (s.get('inflate_shard_ms'), s['inflate_projected_speedup']) for n, s in v['virtual_shards'].items()}, v['roundtrip_ok']) for k, v in d['mixed'].items() if isinstance(v, dict)}"
 for r in 1 2; do
