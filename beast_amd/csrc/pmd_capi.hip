@@ -397,12 +397,14 @@ int inflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
             if (ordered && !(order = bpmd_internal_lane_order(d_in_len, n_msgs, s, &keys))) return BPMD_R_HIP_ERROR;
             if (ordered && long_split && m == 0 && !hist) {
                 // long payloads: block-parallel, or one wave each
-                // (block-parallel: above a lane's share of the batch, from 2 KiB
+                // (block-parallel: above 1.25 lanes' share of the batch, from 2 KiB
                 // compressed; DESIGN.md 4.1c.  One 8-way C4 shard at 50 / 100 /
-                // 150 / 200 %: 9.2 / 8.4-8.9 / 8.3 / 10.5 ms, round 4)
+                // 150 / 200 %: 9.2 / 8.4-8.9 / 8.3 / 10.5 ms; C4 projected 4- and
+                // 8-way speedups at 100 / 125 / 150 %: 3.29-3.30 and 5.29 / 3.36-3.46
+                // and 5.30-5.36 / 2.81-2.95 and 5.39-5.45, round 4)
                 static const uint32_t share_pct = [] {
                     const char* e = getenv("BPMD_LONG_SHARE_PCT");
-                    return e ? (uint32_t)strtoul(e, nullptr, 10) : 100u;
+                    return e ? (uint32_t)strtoul(e, nullptr, 10) : 125u;
                 }();
                 if (!(nlong = bp_ok ? bpmd_internal_lane_long_split(d_in_len, keys, n_msgs, wgs * 64u, 2048u, share_pct, s)
                                     : bpmd_internal_lane_long_split(d_in_len, keys, n_msgs, wgs * 64u, 4096u, 200u, s)))
