@@ -19,6 +19,10 @@ def test_connection_random_cuts(kind, level, mem):
     Z.case_connection_random_cuts(make, kind, level, mem)
 
 
+def test_foreign_encoder_connection():
+    Z.case_foreign_payloads(make)
+
+
 def test_output_room_one_byte():
     Z.case_output_room_one_byte(make, n_calls=1500)
 

@@ -244,6 +244,20 @@ def case_connection_random_cuts(make, kind, level, mem):
         compare(make, stream, calls, label=f"{kind} L{level} m{mem} t{trial}")
 
 
+def case_foreign_payloads(make):
+    """A connection whose peer is another encoder (CPython's zlib, no context
+    takeover): payloads with mid-message none / block / sync / full flushes and
+    zlib's strategies (tests/foreign.py), each followed by 00 00 FF FF, under
+    random cuts and output rooms."""
+    from tests.foreign import foreign_payloads
+    rng = random.Random("foreign")
+    pays, _, _ = foreign_payloads(21, 24)
+    stream = b"".join(p + EB for p in pays)
+    for trial in range(3):
+        calls = random_calls(rng, len(stream), rng.choice([5, 40, 160]), [4096, 1 << 16, 300, 7, 1, 258])
+        compare(make, stream, calls, label=f"foreign t{trial}")
+
+
 def case_output_room_one_byte(make, n_calls=3000):
     # memLevel 9: blocks of up to 32 Ki symbols; output handed out a byte at a time
     msgs = msgs_of("corpus1", [20000], seed=5)
