@@ -23,7 +23,8 @@ reference's own zlib 1.3.1 compiled from its sources (oracle/_ref, when
 present).
 
 Launch:  python bench.py [--gpus N --steps K --warmup W]
-N > 1 runs under torch.distributed.run: every rank works on its own 64 Ki
+N > 1 runs under torch.distributed.run (started here as a child process when
+no launcher set WORLD_SIZE; under one, WORLD_SIZE must equal N): every rank works on its own 64 Ki
 messages (independent streams under no_context_takeover), so there is no
 collective on the data path; scaling is weak.  Timing is barrier +
 synchronize on both sides, max over ranks.
@@ -416,6 +417,39 @@ def mixed_legs(args, rank, world, timer, dev):
     return out
 
 
+def launch_cmd(argv, n, port, python=sys.executable, script=None):
+    """The command that runs this bench as N ranks of one node (one process
+    per GPU, the driver's own form): torch.distributed.run over 127.0.0.1,
+    the same bench arguments (--gpus included, so every rank checks WORLD_SIZE
+    against it)."""
+    return [python, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", script or os.path.abspath(__file__), *argv]
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def maybe_launch(args, argv):
+    """`--gpus N` without a launcher: start N ranks under torch.distributed.run
+    as a CHILD process (nothing here has touched the GPU yet; no exec) and
+    return its exit code.  Under a launcher, WORLD_SIZE must equal N.
+    Returns None when this process is itself the (only or a) rank."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != args.gpus:
+            log(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}")
+            return 2
+        return None
+    if args.gpus <= 1:
+        return None
+    import subprocess
+    return subprocess.run(launch_cmd(argv, args.gpus, _free_port())).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -433,6 +467,9 @@ def main():
     ap.add_argument("--c4-msgs", type=int, default=C4_MSGS, help="configs[3] batch (all ranks together)")
     ap.add_argument("--c5-msgs", type=int, default=C5_MSGS, help="configs[4] batch (all ranks together)")
     args = ap.parse_args()
+    rc = maybe_launch(args, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
