@@ -38,6 +38,8 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
                                         uint32_t* out_len, int32_t* status, uint32_t raw, const uint32_t* order,
                                         const uint32_t* nlong, hipStream_t s);
 extern "C" void bpmd_internal_bp_release(hipStream_t s);
+extern "C" int bpmd_internal_bp_reserve(hipStream_t s, unsigned long long in_bytes, unsigned long long out_bytes,
+                                        unsigned long long msgs);
 extern "C" int bpmd_internal_inflate_wave_ordered(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                                   uint32_t n, uint8_t* out, const uint64_t* out_off,
                                                   const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
@@ -307,6 +309,25 @@ extern "C" int bpmd_init(void)
     if (g_init_devices & bit) return BPMD_R_OK;
     if (bpmd_internal_init_fixed() != 0) return BPMD_R_HIP_ERROR;
     g_init_devices |= bit;
+    return BPMD_R_OK;
+}
+
+// The block-parallel path runs on the caller's stream (batches below 32 Ki
+// messages, forced mode) or on its side stream (work-queue batches): both
+// get the capacity.
+extern "C" int bpmd_inflate_reserve(void* stream, uint64_t in_bytes, uint64_t out_bytes, uint32_t n_long)
+{
+    int r = bpmd_init();
+    if (r) return r;
+    const hipStream_t s = (hipStream_t)stream;
+    std::mutex* mu = stream_mutex(s);
+    if (!mu) return BPMD_R_HIP_ERROR;
+    std::lock_guard<std::mutex> launch(*mu);
+    Side sd;
+    if (!side_for(s, sd)) return BPMD_R_HIP_ERROR;
+    if (bpmd_internal_bp_reserve(s, in_bytes, out_bytes, n_long) ||
+        bpmd_internal_bp_reserve(sd.side, in_bytes, out_bytes, n_long))
+        return BPMD_R_HIP_ERROR;
     return BPMD_R_OK;
 }
 

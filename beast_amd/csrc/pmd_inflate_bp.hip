@@ -45,6 +45,7 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -159,6 +160,23 @@ __global__ void bp_totals_kernel(const uint32_t* __restrict__ regions, const uin
     }
 }
 
+// diagnostics (bpmd_diag_bp_counters): [0] payloads resolved, [1] segments
+// on their chains, [2] payloads sent to the wave kernel by the resolve (a
+// segment outgrew its slot), [3] payloads sent to it by bp_fit_kernel (over
+// the stream's workspace capacity); with -DBPMD_BP_DIAG
+// (contended atomics: timing changes) also [4] regions scanned, [5] found a
+// stored block, [6] searched for dynamic headers, [7] full dynamic-header
+// checks, [8-10] scan cycles staging / stored search / dynamic search
+#ifdef BPMD_BP_DIAG
+#define BP_DIAG(x) x
+#else
+#define BP_DIAG(x)
+#endif
+__device__ unsigned long long g_bp_diag[12];
+// the last payload that fell back to the wave kernel (bpmd_diag_bp_fallback):
+// message, segment (task - first task), segment status, symbols, slot symbols
+__device__ uint32_t g_bp_fb[8];
+
 // Without a read-back the decode workspace has a fixed capacity (tasks,
 // symbol words): the long payloads that fit are a prefix of the order
 // (the sums only grow), the rest go to the wave kernel's list.  fit[0] =
@@ -190,22 +208,11 @@ bp_fit_kernel(const uint32_t* __restrict__ nlong, const uint32_t* __restrict__ r
         tot->words = n ? word_base[n - 1] + words[n - 1] : 0ull;
     }
     for (uint32_t i = nfit + threadIdx.x; i < nl; i += blockDim.x) fb_list[atomicAdd(fb_count, 1u)] = order[i];
+    // capacity spills (bpmd_diag_bp_counters [3]): payloads the workspace
+    // could not take this call
+    if (threadIdx.x == 0 && nl > nfit) atomicAdd(&g_bp_diag[3], (unsigned long long)(nl - nfit));
 }
 
-// diagnostics (bpmd_diag_bp_counters): [0] payloads resolved, [1] segments
-// on their chains, [2] payloads sent to the wave kernel; with -DBPMD_BP_DIAG
-// (contended atomics: timing changes) also [4] regions scanned, [5] found a
-// stored block, [6] searched for dynamic headers, [7] full dynamic-header
-// checks, [8-10] scan cycles staging / stored search / dynamic search
-#ifdef BPMD_BP_DIAG
-#define BP_DIAG(x) x
-#else
-#define BP_DIAG(x)
-#endif
-__device__ unsigned long long g_bp_diag[12];
-// the last payload that fell back to the wave kernel (bpmd_diag_bp_fallback):
-// message, segment (task - first task), segment status, symbols, slot symbols
-__device__ uint32_t g_bp_fb[8];
 
 // ------------------------------------------------------------------ scan
 __device__ __forceinline__ uint32_t wave_lane() { return threadIdx.x & 63u; }
@@ -907,11 +914,17 @@ bp_resolve_kernel(const uint32_t* __restrict__ order, const uint32_t* __restrict
 // ------------------------------------------------------------------ driver
 // Long payloads order[0, *nlong) of a batch (pmd_capi.hip inflate_impl); the
 // rest of the batch is the caller's.  n: the batch's message count (bounds
-// nlong).  Everything is enqueued on s and nothing waits on the device: the
-// decode workspace has a per-(device, stream) capacity, the long payloads
-// that do not fit it go to the wave kernel (bp_fit_kernel), and each call's
-// totals are copied to pinned memory so that a later call grows the capacity
-// to them (the growth itself frees the old block only once s is idle).
+// nlong).  The decode workspace has a per-(device, stream) capacity:
+//   * the first call on a stream sizes it to that call's needs (one read-back
+//     of the totals, the only wait of the path), or bpmd_inflate_reserve()
+//     sets it beforehand with no wait at all;
+//   * later calls only enqueue: long payloads that do not fit go to the wave
+//     kernel (bp_fit_kernel, counted in bpmd_diag_bp_counters [3]) and each
+//     call's totals are copied to pinned memory, so that a later call grows
+//     the capacity to them once that copy has completed;
+//   * growth is bounded by the device's free memory, and a workspace that
+//     cannot be allocated falls back to the last capacity that could (or to
+//     none: every long payload then takes the wave kernel), never an error.
 namespace {
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 struct BpCaps {
@@ -920,11 +933,62 @@ struct BpCaps {
     unsigned long long tasks, words;   // decode workspace capacity
     bpmd::bp::Totals* seen;            // pinned: the totals of the last call
     hipEvent_t ev;                     // recorded after that copy
-    bool pending;
+    bool pending;                      // ev recorded, not yet consumed
+    bool sized;                        // capacity set (first call or reserve)
 };
 std::mutex g_bp_mu;
 std::vector<BpCaps> g_bp_caps;
-constexpr unsigned long long BP_TASKS0 = 1ull << 16, BP_WORDS0 = 1ull << 25;   // first capacity: 64 Ki tasks, 64 MiB
+std::atomic<int> g_bp_fail{0};   // diagnostics: decode-workspace allocations to fail
+
+uint8_t* dw_alloc(hipStream_t s, size_t bytes)
+{
+    if (g_bp_fail.load() > 0 && g_bp_fail.fetch_sub(1) > 0) return nullptr;
+    return (uint8_t*)bpmd_internal_scratch(s, bytes, 11);
+}
+
+// the entry of (device, stream), created zeroed; nullptr when the pinned
+// totals or the event cannot be made.  Caller holds g_bp_mu.
+BpCaps* caps_for(int dev, hipStream_t s)
+{
+    for (auto& e : g_bp_caps)
+        if (e.dev == dev && e.s == s) return &e;
+    BpCaps e{dev, s, 0, 0, nullptr, nullptr, false, false};
+    if (hipHostMalloc((void**)&e.seen, sizeof(bpmd::bp::Totals), hipHostMallocDefault) != hipSuccess) return nullptr;
+    e.seen->tasks = e.seen->words = 0;
+    if (hipEventCreateWithFlags(&e.ev, hipEventDisableTiming) != hipSuccess) {
+        (void)hipHostFree(e.seen);
+        return nullptr;
+    }
+    g_bp_caps.push_back(e);
+    return &g_bp_caps.back();
+}
+
+// decode workspace bytes for a capacity (n: the batch's message count)
+inline size_t dw_bytes(unsigned long long tasks, unsigned long long words, uint32_t n)
+{
+    using namespace bpmd::bp;
+    const size_t d_res = al256(sizeof(SegTask) * tasks), d_fb = al256(d_res + sizeof(SegRes) * tasks),
+                 d_map = al256(d_fb + 4ull * n), d_mark = al256(d_map + 4ull * tasks),
+                 d_sym = al256(d_mark + 4ull * n);
+    return al256(d_sym + 2ull * (words + SYM_GUARD + 64));
+}
+
+// a capacity of t tasks and w words plus a quarter, within half the free memory
+void grow_to(BpCaps* c, unsigned long long t, unsigned long long w)
+{
+    unsigned long long nt = c->tasks, nw = c->words;
+    if (t > nt) nt = t + t / 4;
+    if (w > nw) nw = w + w / 4;
+    if (nt > 0xffffffffull) nt = 0xffffffffull;
+    size_t fr = 0, tot = 0;
+    if ((nt != c->tasks || nw != c->words) && hipMemGetInfo(&fr, &tot) == hipSuccess) {
+        const unsigned long long budget = fr / 2, per_task = sizeof(bpmd::bp::SegTask) + sizeof(bpmd::bp::SegRes) + 4;
+        if (nt * per_task > budget) nt = budget / per_task;
+        if (2 * nw + nt * per_task > budget) nw = (budget - nt * per_task) / 2;
+    }
+    c->tasks = nt > c->tasks ? nt : c->tasks;
+    c->words = nw > c->words ? nw : c->words;
+}
 }  // namespace
 
 // frees the pinned totals and event of a stream about to be destroyed
@@ -944,6 +1008,27 @@ extern "C" void bpmd_internal_bp_release(hipStream_t s)
         }
 }
 
+// bpmd_inflate_reserve (pmd_capi.hip): a capacity for batches whose long
+// payloads total at most in_bytes of input, out_bytes of output capacity and
+// msgs payloads -- bp_stats_kernel's bounds: regions of >= R_MIN bytes, at
+// most one more per payload; slot words 2 (len + regions) x 1.25 x
+// min(cap / len, 4) + SLACK per region + the guard per payload.
+extern "C" int bpmd_internal_bp_reserve(hipStream_t s, unsigned long long in_bytes, unsigned long long out_bytes,
+                                        unsigned long long msgs)
+{
+    using namespace bpmd::bp;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return (int)hipErrorNoDevice;
+    const unsigned long long t = in_bytes / R_MIN + msgs;
+    const unsigned long long w = (5 * out_bytes) / 2 + (10ull + SLACK) * t + (SYM_GUARD + 64ull) * msgs;
+    std::lock_guard<std::mutex> lk(g_bp_mu);
+    BpCaps* c = caps_for(dev, s);
+    if (!c) return (int)hipErrorOutOfMemory;
+    grow_to(c, t, w);
+    c->sized = true;
+    return 0;
+}
+
 extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n,
                                         uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                                         uint32_t* out_len, int32_t* status, uint32_t raw, const uint32_t* order,
@@ -957,31 +1042,20 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
     unsigned long long cap_tasks = 0, cap_words = 0;
     Totals* seen = nullptr;
     hipEvent_t ev = nullptr;
+    bool cold = false;
     {
         std::lock_guard<std::mutex> lk(g_bp_mu);
-        BpCaps* c = nullptr;
-        for (auto& e : g_bp_caps)
-            if (e.dev == dev && e.s == s) c = &e;
-        if (!c) {
-            BpCaps e{dev, s, BP_TASKS0, BP_WORDS0, nullptr, nullptr, false};
-            if (hipHostMalloc((void**)&e.seen, sizeof(Totals), hipHostMallocDefault) != hipSuccess)
-                return (int)hipErrorOutOfMemory;
-            if (hipEventCreateWithFlags(&e.ev, hipEventDisableTiming) != hipSuccess) return (int)hipErrorUnknown;
-            g_bp_caps.push_back(e);
-            c = &g_bp_caps.back();
-        }
+        BpCaps* c = caps_for(dev, s);
+        if (!c) return (int)hipErrorOutOfMemory;
         if (c->pending && hipEventQuery(c->ev) == hipSuccess) {
             c->pending = false;
-            const unsigned long long t = c->seen->tasks, w = c->seen->words;
-            if (t > c->tasks) c->tasks = t + t / 4;
-            if (w > c->words) c->words = w + w / 4;
+            grow_to(c, c->seen->tasks, c->seen->words);
         }
-        if (c->tasks > 0xffffffffull) c->tasks = 0xffffffffull;
+        cold = !c->sized;
         cap_tasks = c->tasks;
         cap_words = c->words;
         seen = c->seen;
         ev = c->ev;
-        c->pending = true;
     }
     // per-payload workspace (scratch block 10): stats, regions, words, their
     // exclusive sums, totals, fit, queues, scan temp
@@ -998,14 +1072,7 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
     // q: [0] scan queue, [1] resolve queue, [2] fallback count, [3] seg queue,
     // [4-5] long bytes, [6] payloads that fit, [7] their tasks
     uint8_t* ws = (uint8_t*)bpmd_internal_scratch(s, sz, 10);
-    // decode workspace (scratch block 11), sized by the capacity: tasks,
-    // results, fallback list, region map, marks, symbols
-    const size_t d_tasks = 0, d_res = al256(d_tasks + sizeof(SegTask) * cap_tasks),
-                 d_fb = al256(d_res + sizeof(SegRes) * cap_tasks), d_map = al256(d_fb + 4ull * n),
-                 d_mark = al256(d_map + 4ull * cap_tasks), d_sym = al256(d_mark + 4ull * n),
-                 dsz = al256(d_sym + 2ull * (cap_words + SYM_GUARD + 64));
-    uint8_t* dw = (uint8_t*)bpmd_internal_scratch(s, dsz, 11);
-    if (!ws || !dw) return (int)hipErrorOutOfMemory;
+    if (!ws) return (int)hipErrorOutOfMemory;
     Stat* st = (Stat*)(ws + o_st);
     uint32_t* reg = (uint32_t*)(ws + o_reg);
     uint32_t* tbase = (uint32_t*)(ws + o_tb);
@@ -1014,16 +1081,9 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
     Totals* dtot = (Totals*)(ws + o_tot);
     uint32_t* q = (uint32_t*)(ws + o_q);
     void* tmp = ws + o_tmp;
-    SegTask* tasks = (SegTask*)(dw + d_tasks);
-    SegRes* res = (SegRes*)(dw + d_res);
-    uint32_t* fb = (uint32_t*)(dw + d_fb);
-    uint16_t* sym = (uint16_t*)(dw + d_sym);
-    uint32_t* rmap = (uint32_t*)(dw + d_map);
-    uint32_t* marked = (uint32_t*)(dw + d_mark);
     unsigned long long* total = (unsigned long long*)(q + 4);
     uint32_t* fit = q + 6;
-    if (hipMemsetAsync(q, 0, 64, s) != hipSuccess || hipMemsetAsync(marked, 0, 4ull * n, s) != hipSuccess)
-        return (int)hipErrorUnknown;
+    if (hipMemsetAsync(q, 0, 64, s) != hipSuccess) return (int)hipErrorUnknown;
     hipLaunchKernelGGL(bp_sum_kernel, dim3(n / 256 + 1 < 1024 ? n / 256 + 1 : 1024), dim3(256), 0, s, in_len, order,
                        nlong, n, total);
     // BPMD_BP_SEGS (diagnostics): target segments per lane of the chip
@@ -1039,13 +1099,77 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
     if (hipcub::DeviceScan::ExclusiveSum(tmp, t1, reg, tbase, (int)n, s) != hipSuccess ||
         hipcub::DeviceScan::ExclusiveSum(tmp, t2, words, wbase, (int)n, s) != hipSuccess)
         return (int)hipErrorUnknown;
+    if (cold) {
+        // the stream's first call: its own totals, read back once
+        hipLaunchKernelGGL(bp_totals_kernel, dim3(1), dim3(64), 0, s, reg, tbase, words, wbase, n, dtot);
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpyAsync(seen, dtot, sizeof(Totals), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return (int)hipErrorUnknown;
+        std::lock_guard<std::mutex> lk(g_bp_mu);
+        BpCaps* c = caps_for(dev, s);
+        if (!c) return (int)hipErrorOutOfMemory;
+        grow_to(c, seen->tasks, seen->words);
+        c->sized = true;
+        cap_tasks = c->tasks;
+        cap_words = c->words;
+    }
+    // decode workspace (scratch block 11), sized by the capacity: tasks,
+    // results, fallback list, region map, marks, symbols.  A block that
+    // cannot be had: the capacity it replaces, else none.
+    uint8_t* dw = dw_alloc(s, dw_bytes(cap_tasks, cap_words, n));
+    if (!dw) {
+        (void)hipGetLastError();   // clear the allocation error
+        unsigned long long pt = 0, pw = 0;
+        {
+            std::lock_guard<std::mutex> lk(g_bp_mu);
+            BpCaps* c = caps_for(dev, s);
+            if (c) {
+                pt = c->tasks = c->tasks == cap_tasks ? c->tasks / 2 : c->tasks;
+                pw = c->words = c->words == cap_words ? c->words / 2 : c->words;
+            }
+        }
+        cap_tasks = pt;
+        cap_words = pw;
+        for (;;) {
+            if (cap_words < (1ull << 16)) cap_tasks = cap_words = 0;
+            dw = dw_alloc(s, dw_bytes(cap_tasks, cap_words, n));
+            if (dw) break;
+            (void)hipGetLastError();
+            if (cap_words == 0) return (int)hipErrorOutOfMemory;   // not even the lists
+            cap_tasks /= 2;
+            cap_words /= 2;
+        }
+        std::lock_guard<std::mutex> lk(g_bp_mu);
+        BpCaps* c = caps_for(dev, s);
+        if (c) {
+            c->tasks = cap_tasks;
+            c->words = cap_words;
+        }
+    }
+    const size_t d_tasks = 0, d_res = al256(d_tasks + sizeof(SegTask) * cap_tasks),
+                 d_fb = al256(d_res + sizeof(SegRes) * cap_tasks), d_map = al256(d_fb + 4ull * n),
+                 d_mark = al256(d_map + 4ull * cap_tasks), d_sym = al256(d_mark + 4ull * n);
+    SegTask* tasks = (SegTask*)(dw + d_tasks);
+    SegRes* res = (SegRes*)(dw + d_res);
+    uint32_t* fb = (uint32_t*)(dw + d_fb);
+    uint16_t* sym = (uint16_t*)(dw + d_sym);
+    uint32_t* rmap = (uint32_t*)(dw + d_map);
+    uint32_t* marked = (uint32_t*)(dw + d_mark);
+    if (hipMemsetAsync(marked, 0, 4ull * n, s) != hipSuccess) return (int)hipErrorUnknown;
     hipLaunchKernelGGL(bp_fit_kernel, dim3(1), dim3(256), 0, s, nlong, reg, tbase, words, wbase, n, cap_tasks,
                        cap_words, order, fit, dtot, fb, q + 2);
-    // the totals for a later call (pinned, no wait here)
+    // the totals for a later call (pinned, no wait here); the event counts
+    // only once it is recorded
     if (hipGetLastError() != hipSuccess ||
         hipMemcpyAsync(seen, dtot, sizeof(Totals), hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipEventRecord(ev, s) != hipSuccess)
         return (int)hipErrorUnknown;
+    {
+        std::lock_guard<std::mutex> lk(g_bp_mu);
+        BpCaps* c = caps_for(dev, s);
+        if (c) c->pending = true;
+    }
     // scan: one wave per region, SCAN_WAVES waves per workgroup, ~3
     // workgroups per CU by LDS; then the slots, one wave per payload
     hipLaunchKernelGGL(bp_region_map_kernel, dim3((n + 255) / 256), dim3(256), 0, s, fit, reg, tbase, rmap);
@@ -1070,6 +1194,9 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
     return bpmd_internal_inflate_wave_ordered(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, raw,
                                               nullptr, fb, q + 2, s);
 }
+
+// diagnostics (tests): the next k decode-workspace allocations fail
+extern "C" void bpmd_diag_bp_fail_alloc(int k) { g_bp_fail.store(k); }
 
 extern "C" int bpmd_diag_bp_fallback(uint32_t* out8)
 {

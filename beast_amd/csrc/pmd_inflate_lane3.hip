@@ -1636,8 +1636,9 @@ extern "C" const uint32_t* bpmd_internal_lane_order(const uint32_t* in_len, uint
 // kernel, which decodes one message with 64 lanes, or to the block-parallel
 // decoder, which cuts it at block starts.  "Longer than its share":
 // compressed length above share_pct % of the batch's compressed bytes per
-// resident lane (block-parallel: 100 %, so the work queue ends near the
-// per-lane share; wave kernel: 200 %), and never below min_thr.  The count is computed on the device from the sorted keys, so the
+// resident lane (block-parallel: 125 % by default, BPMD_LONG_SHARE_PCT, so
+// the work queue ends near the per-lane share; wave kernel: 200 %; the
+// values live in pmd_capi.hip inflate_impl), and never below min_thr.  The count is computed on the device from the sorted keys, so the
 // call stays asynchronous: split[0] = total compressed bytes (u64),
 // split[2] = number of long payloads = a prefix of the longest-first order.
 namespace bpmd {

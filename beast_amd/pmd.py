@@ -63,6 +63,8 @@ def lib():
         L.bpmd_deflate_batch.argtypes = [ctypes.POINTER(_Cfg), vp, vp, vp, ctypes.c_uint32, vp, vp, vp, vp, vp, vp]
         L.bpmd_diag_set_wave_walk.argtypes = [ctypes.c_int]
         L.bpmd_diag_bp_counters.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+        L.bpmd_inflate_reserve.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32]
+        L.bpmd_inflate_reserve.restype = ctypes.c_int
         L.bpmd_shard_ranges.argtypes = [vp, ctypes.c_uint32, ctypes.c_int, vp]
         L.bpmd_inflate_batch_multi.argtypes = [ctypes.POINTER(_Cfg), vp, ctypes.c_int, vp]
         L.bpmd_deflate_batch_multi.argtypes = [ctypes.POINTER(_Cfg), vp, ctypes.c_int, vp]
@@ -194,6 +196,22 @@ def inflate_batch(src: Batch, out_cap, window_bits: int = 15, raw: bool = False,
                                 _ptr(out_off), _ptr(cap), _ptr(out_len), _ptr(status), _stream_handle(stream)),
            "bpmd_inflate_batch")
     return Result(Batch(out, out_off, out_len), cap, status)
+
+
+def inflate_reserve(in_bytes: int, out_bytes: int, n_long: int, stream=None) -> None:
+    """bpmd_inflate_reserve: size `stream`'s block-parallel decode workspace
+    for batches whose long payloads total at most in_bytes / out_bytes /
+    n_long, so that no call on it waits to size it (include/beast_pmd.h)."""
+    _check(lib().bpmd_inflate_reserve(_stream_handle(stream), in_bytes, out_bytes, n_long), "bpmd_inflate_reserve")
+
+
+def bp_counters(reset: bool = True) -> list:
+    """bpmd_diag_bp_counters: [0] payloads resolved block-parallel, [1] their
+    segments, [2] resolve fallbacks to the wave kernel, [3] capacity spills
+    to it (pmd_inflate_bp.hip)."""
+    c = (ctypes.c_ulonglong * 12)()
+    _check(lib().bpmd_diag_bp_counters(c, 1 if reset else 0), "bpmd_diag_bp_counters")
+    return list(c)
 
 
 def deflate_batch(src: Batch, level: int = 6, window_bits: int = 15, mem_level: int = 4, strategy: int = 0,

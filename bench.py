@@ -398,13 +398,9 @@ def mixed_legs(args, rank, world, timer, dev):
             vs = {}
             for parts in (2, 4, 8):
                 dt, it = [], []
-                # two warmup calls per share: the block-parallel workspace of a
-                # stream grows one call after a call that needed more (no
-                # read-back, pmd_inflate_bp.hip), and a share's first call may be
-                # the one that needs more
                 for a, b in shard.byte_balanced_ranges(lens, parts):
-                    dt.append(timer.run(lambda: deflate_step(a, b), steps, 2)[0])
-                    it.append(timer.run(lambda: inflate_step(a, b), steps, 2)[0])
+                    dt.append(timer.run(lambda: deflate_step(a, b), steps, 1)[0])
+                    it.append(timer.run(lambda: inflate_step(a, b), steps, 1)[0])
                 vs[str(parts)] = {
                     "deflate_shard_ms": [round(t * 1e3, 3) for t in dt],
                     "inflate_shard_ms": [round(t * 1e3, 3) for t in it],

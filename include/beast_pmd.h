@@ -28,7 +28,11 @@
  *   - a call that needs more device workspace than its stream's pool holds
  *     (work queues, chunk scratch, block-parallel decode workspace) grows
  *     the pool, and freeing the smaller block waits for `stream` to drain;
- *     a stream that repeats one batch shape grows it only on the first calls.
+ *     a stream that repeats one batch shape grows it only on the first calls;
+ *   - the first inflate call on a stream that decodes long payloads
+ *     block-parallel reads back that batch's workspace totals once (so the
+ *     first call already runs the fast path), unless bpmd_inflate_reserve()
+ *     sized the stream before.
  * Concurrent calls from several host threads on one stream are serialised
  * per stream.
  */
@@ -112,6 +116,16 @@ int bpmd_inflate_batch(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t*
                        const uint32_t* d_in_len, uint32_t n_msgs, uint8_t* d_out,
                        const uint64_t* d_out_off, const uint32_t* d_out_cap,
                        uint32_t* d_out_len, int32_t* d_status, void* stream);
+
+/* Workspace for the block-parallel decode of long payloads on `stream`
+ * (no Beast counterpart: the reference decodes on the caller's thread).  Sizes
+ * the stream's capacity for batches whose long payloads total at most
+ * in_bytes of compressed input, out_bytes of output capacity and n_long
+ * payloads, so that no later call on the stream waits to size it; a long
+ * payload that does not fit a stream's capacity is still decoded exactly, by
+ * the slower wave kernel.  The capacity never exceeds half the device's free
+ * memory.  Optional: without it the stream's first such call sizes it. */
+int bpmd_inflate_reserve(void* stream, uint64_t in_bytes, uint64_t out_bytes, uint32_t n_long);
 
 /* Batched deflate of independent messages into permessage-deflate payloads
  * (replaces one zo.write(zs, Flush::none) ... zo.write(zs, Flush::block),

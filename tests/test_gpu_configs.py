@@ -141,8 +141,9 @@ def test_c4_work_queue_batch():
 
 
 def test_c4_long_payloads_split_from_lanes():
-    """A work-queue batch whose longest payloads exceed half the batch's
-    compressed bytes per resident lane (and 2 KiB): those are decoded
+    """A work-queue batch whose longest payloads exceed 125 % of the batch's
+    compressed bytes per resident lane (and 2 KiB; the value lives in
+    pmd_capi.hip inflate_impl, BPMD_LONG_SHARE_PCT): those are decoded
     block-parallel (pmd_inflate_bp.hip) on a side stream from the
     longest-first order while the lane kernel takes the rest (pmd_capi.hip
     inflate_impl, bpmd_internal_lane_long_split; the wave kernel when

@@ -216,3 +216,97 @@ def test_c5_payload_with_false_stored_candidate(level):
     assert int(r.status[0]) == 0 and int(r.out.len[0]) == 65536
     assert torch.equal(r.out.data[:65536], src.data[:65536])
     assert c[0] == 1 and c[1] >= 8 and c[2] == 0, list(c)[:3]   # one payload, its segments, no fallback
+
+
+# ---------------------------------------------------- workspace sizing (r05)
+# A stream's block-parallel decode workspace is sized on its first call (one
+# read-back) or by bpmd_inflate_reserve; payloads over the capacity are
+# spilled to the wave kernel (counter [3]) and the capacity grows for the
+# next call; a workspace that cannot be allocated falls back to a smaller
+# one.  Each test releases its stream's pools so the next one starts cold.
+
+def _c5_like(n, seed, level=1):
+    import torch
+    pmd = _pmd()
+    raw, off, ln = synth.make_batch("binary", np.full(n, 65536, np.uint32), seed=seed)
+    src = pmd.Batch.from_arrays(raw, off.astype(np.int64), ln.astype(np.int32))
+    d = pmd.deflate_batch(src, level=level)
+    torch.cuda.synchronize()
+    assert int((d.status != 0).sum()) == 0
+    return src, pmd.Batch(d.out.data, d.out.off, d.out.len), torch.from_numpy(ln.astype(np.int32)).cuda()
+
+
+def _on_fresh_stream(fn):
+    import ctypes
+    import torch
+    pmd = _pmd()
+    assert pmd.lib().bpmd_set_inflate_kernel(0) == 0
+    st = torch.cuda.Stream()
+    try:
+        with torch.cuda.stream(st):
+            return fn(st)
+    finally:
+        st.synchronize()
+        pmd.lib().bpmd_internal_scratch_release(ctypes.c_void_p(st.cuda_stream))
+
+
+def _call(st, comp, cap, src):
+    import torch
+    pmd = _pmd()
+    out = torch.empty_like(src.data)
+    pmd.bp_counters(reset=True)
+    r = pmd.inflate_batch(comp, cap, out=out, out_off=src.off, stream=st)
+    st.synchronize()
+    c = pmd.bp_counters(reset=True)
+    ok = int((r.status != 0).sum()) == 0 and torch.equal(r.out.len, src.len) and torch.equal(out, src.data)
+    return ok, c
+
+
+def test_first_call_on_a_fresh_stream_takes_no_fallback():
+    """The stream's first C5-shaped call already decodes every long payload
+    block-parallel: no capacity spill, no resolve fallback."""
+    src, comp, cap = _c5_like(2048, 0x5EED0061)
+
+    def body(st):
+        ok, c = _call(st, comp, cap, src)
+        assert ok
+        assert c[0] == 2048 and c[2] == 0 and c[3] == 0, c[:4]
+        ok, c = _call(st, comp, cap, src)
+        assert ok and c[0] == 2048 and c[2] == 0 and c[3] == 0, c[:4]
+    _on_fresh_stream(body)
+
+
+def test_reserved_too_small_spills_then_grows():
+    """A reserve far below the batch: the fitting prefix decodes
+    block-parallel, the rest through the wave kernel, all exact; the next
+    call has grown to the batch and spills nothing."""
+    src, comp, cap = _c5_like(512, 0x5EED0062)
+    pmd = _pmd()
+
+    def body(st):
+        pmd.inflate_reserve(65536, 65536, 1, stream=st)
+        ok, c = _call(st, comp, cap, src)
+        assert ok and c[3] > 0 and c[0] + c[3] == 512, c[:4]
+        ok, c = _call(st, comp, cap, src)
+        assert ok and c[0] == 512 and c[2] == 0 and c[3] == 0, c[:4]
+    _on_fresh_stream(body)
+
+
+def test_failed_workspace_allocation_falls_back():
+    """The first three decode-workspace allocations fail: the call keeps a
+    smaller workspace (exact output, spills to the wave kernel), and the next
+    call on the same stream grows it again and decodes everything
+    block-parallel."""
+    src, comp, cap = _c5_like(512, 0x5EED0063)
+    pmd = _pmd()
+
+    def body(st):
+        pmd.lib().bpmd_diag_bp_fail_alloc(3)
+        try:
+            ok, c = _call(st, comp, cap, src)
+        finally:
+            pmd.lib().bpmd_diag_bp_fail_alloc(0)
+        assert ok and c[3] > 0, c[:4]
+        ok, c = _call(st, comp, cap, src)
+        assert ok and c[0] == 512 and c[3] == 0, c[:4]
+    _on_fresh_stream(body)
