@@ -107,6 +107,56 @@ __device__ __forceinline__ unsigned ring_at(uint32_t e)
     const uint32_t k = e % RING;
     return k < 8 ? O_HIST + 8 * k : O_CLS + 8 * (k - 8);
 }
+
+// Per-lane LDS addressing.  Default: one lane's area is contiguous, lanes
+// STRIDE bytes apart (158 dwords, an even count: same-offset accesses of
+// lanes l and l + 16 share a bank, and table lookups at lane-dependent
+// offsets collide at random).  BPMD3_ILV=1 interleaves the 64 areas by
+// dword -- dword w of lane l at 256 w + 4 l of the workgroup's block -- so
+// every lane stays in bank l mod 32 whatever the offset (MI355X_MICROARCH.md
+// LDS: ds_read_b32 serves lanes 0-31 and 32-63 one cycle each): C2's
+// SQ_LDS_BANK_CONFLICT 36.5 M -> 0, but each table lookup's address costs two
+// more VALU instructions (SQ_INSTS_VALU 471 M -> 501 M) and the decoder is
+// issue-bound, not LDS-bound (SQ_WAIT_INST_LDS 1.4 M of 1 428 M wave
+// cycles): C2 189.4-190.3 (contiguous) vs 184.4-185.3 GiB/s (interleaved),
+// three interleaved runs on one box (profiles/r05b_ab_lds_interleave.log,
+// r05b_c2_sq_interleaved.txt).
+#ifndef BPMD3_ILV
+#define BPMD3_ILV 0
+#endif
+__device__ __forceinline__ uint8_t* lane_area(uint8_t* smem, unsigned lane)
+{
+    return BPMD3_ILV ? smem + 4 * lane : smem + lane * STRIDE;
+}
+// byte b / dword w of the lane's area (T = lane_area())
+__device__ __forceinline__ uint8_t* lb(uint8_t* T, uint32_t b)
+{
+    return BPMD3_ILV ? T + (((b >> 2) << 8) | (b & 3u)) : T + b;
+}
+__device__ __forceinline__ uint32_t* lw(uint8_t* T, uint32_t w)
+{
+    return BPMD3_ILV ? (uint32_t*)(T + (w << 8)) : (uint32_t*)T + w;
+}
+__device__ __forceinline__ uint2 ring_ld(uint8_t* T, uint32_t e)
+{
+    const uint32_t d = ring_at(e) >> 2;
+    return make_uint2(*lw(T, d), *lw(T, d + 1));
+}
+__device__ __forceinline__ void ring_st(uint8_t* T, uint32_t e, uint2 v)
+{
+    const uint32_t d = ring_at(e) >> 2;
+    *lw(T, d) = v.x;
+    *lw(T, d + 1) = v.y;
+}
+// c ? b : a as bitwise selects the compiler cannot turn back into a
+// dynamically indexed array (which it places in scratch memory)
+__device__ __forceinline__ uint2 pick(uint2 a, uint2 b, bool c)
+{
+    uint32_t m = c ? ~0u : 0u;
+    asm volatile("" : "+v"(m));
+    return make_uint2((b.x & m) | (a.x & ~m), (b.y & m) | (a.y & ~m));
+}
+constexpr uint32_t W_HIST = O_HIST / 4, W_LE = O_LE / 4, W_NIB = O_NIB / 4, W_HEAD = O_HEAD / 4, W_TAIL = O_TAIL / 4;
 // Diagnostic build only (-DBPMD_PROF): per-role loop counters, summed over waves:
 // [0] decoder cycles [1] decoder iterations [2] decoder sleeps [3] decoder
 // header iterations [4] expander cycles [5] expander iterations [6] expander sleeps
@@ -212,11 +262,11 @@ __device__ __forceinline__ void expander(uint8_t* T, bool valid, uint32_t m, uin
         }
         // ================================================ take pieces
         if (!exited) {
-            const uint32_t head = lds_load(T + O_HEAD);
+            const uint32_t head = lds_load((uint8_t*)lw(T, W_HEAD));
             compiler_fence();
             uint2 ent[KX];
 #pragma unroll
-            for (int j = 0; j < KX; ++j) ent[j] = *(const uint2*)(T + ring_at(tail + j));
+            for (int j = 0; j < KX; ++j) ent[j] = ring_ld(T, tail + j);
             compiler_fence();
             const uint32_t F = crem ? cq : pos;   // everything before F is stored
             uint32_t k = 0;                       // entries taken this iteration
@@ -229,7 +279,7 @@ __device__ __forceinline__ void expander(uint8_t* T, bool valid, uint32_t m, uin
                     } else {
                         uint2 e = ent[0];
 #pragma unroll
-                        for (int i = 1; i <= j; ++i) e = k == (uint32_t)i ? ent[i] : e;
+                        for (int i = 1; i <= j; ++i) e = pick(e, ent[i], k == (uint32_t)i);
                         if (e.y & TOK_END) {
                             out_len[m] = e.x;
                             const int32_t stt = (int32_t)(int8_t)(e.y & 0xffu);
@@ -325,7 +375,7 @@ __device__ __forceinline__ void expander(uint8_t* T, bool valid, uint32_t m, uin
                     }
                 }
             }
-            lds_store(T + O_TAIL, tail);
+            lds_store((uint8_t*)lw(T, W_TAIL), tail);
         }
         if (!__ballot(worked)) {   // the decoder is behind: leave it the SIMD
             L3_CNT(2);
@@ -483,11 +533,11 @@ __device__ __forceinline__ void expander_seg(uint8_t* T, bool valid, uint32_t m,
         }
         // ================================================ take pieces
         if (!exited || crem != 0 || srem != 0) {
-            const uint32_t head = exited ? tail : lds_load(T + O_HEAD);
+            const uint32_t head = exited ? tail : lds_load((uint8_t*)lw(T, W_HEAD));
             compiler_fence();
             uint2 ent[KX];
 #pragma unroll
-            for (int j = 0; j < KX; ++j) ent[j] = *(const uint2*)(T + ring_at(tail + j));
+            for (int j = 0; j < KX; ++j) ent[j] = ring_ld(T, tail + j);
             compiler_fence();
             const uint32_t F = crem ? cq : srem ? sdst : pos;   // every symbol before F is stored
             uint32_t k = 0;
@@ -500,7 +550,7 @@ __device__ __forceinline__ void expander_seg(uint8_t* T, bool valid, uint32_t m,
                     } else {
                         uint2 e = ent[0];
 #pragma unroll
-                        for (int i = 1; i <= j; ++i) e = k == (uint32_t)i ? ent[i] : e;
+                        for (int i = 1; i <= j; ++i) e = pick(e, ent[i], k == (uint32_t)i);
                         if (e.y & TOK_END) {
                             const uint32_t delta = (e.y >> 8) & 0x1fffffu;
                             bp::SegRes r;
@@ -623,7 +673,7 @@ __device__ __forceinline__ void expander_seg(uint8_t* T, bool valid, uint32_t m,
                     }
                 }
             }
-            if (!exited || k) lds_store(T + O_TAIL, tail);
+            if (!exited || k) lds_store((uint8_t*)lw(T, W_TAIL), tail);
         }
         if (!__ballot(worked)) {
             L3_CNT(2);
@@ -648,8 +698,6 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
                                         uint32_t* __restrict__ qctr, uint32_t s0,
                                         const bp::SegTask* __restrict__ tasks)
 {
-    uint32_t* H = (uint32_t*)(T + O_HIST);
-    uint16_t* LE = (uint16_t*)(T + O_LE);
     const uint32_t tail = raw ? 0u : 4u;
     const int32_t full_status = SEG ? bp::SEG_FULL : raw ? ST_OK : ST_NEED_BUFFERS;
     // segment mode: payload bit of the view's first bit, the view's bits, and
@@ -863,8 +911,8 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
         uint32_t kle[KLIT], ksb[KLIT];
 #pragma unroll
         for (int k = 0; k < KLIT; ++k) {
-            kle[k] = LE[kL[k]];
-            ksb[k] = T[O_LIT + kx[k]];
+            kle[k] = *(const uint16_t*)lb(T, O_LE + 2 * kL[k]);
+            ksb[k] = *lb(T, O_LIT + kx[k]);
         }
         uint32_t ks[KLIT];
 #pragma unroll
@@ -922,7 +970,7 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
         const uint32_t d15 = rev15(w2 >> used);
         const Sym yd = canon_decode<15>(td.Q, d15);
         const uint32_t Ld = yd.L;
-        const uint32_t dsym = T[O_DST + yd.idx];
+        const uint32_t dsym = *lb(T, O_DST + yd.idx);
         const bool invd = yd.inval || dsym >= 30;
         const uint32_t xd = dsym < 4 ? 0u : (dsym >> 1) - 1;
         uint32_t dist = dsym < 4 ? dsym + 1 : (((2u + (dsym & 1)) << xd) + 1);
@@ -1001,7 +1049,7 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
 #endif
         // ---- the input pipeline (the only global memory the decoder touches)
         if (nx_used) pipe();
-        const uint32_t taken = lds_load(T + O_TAIL);
+        const uint32_t taken = lds_load((uint8_t*)lw(T, W_TAIL));
         compiler_fence();
         const bool room = head - taken < RING;
         const bool ring_empty = head == taken;
@@ -1057,21 +1105,18 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
                     } else if (type == 1) {
                         // fixed tables (inflate_stream.ipp:865-930): canonical
                         // order is 256-279 | 0-143 280-287 | 144-255, distances 0-31
-                        uint4* dst4 = (uint4*)T;
 #pragma unroll 1
                         for (int k = 0; k < 20; ++k) {
-                            uint32_t w4[4];
 #pragma unroll
                             for (int j = 0; j < 4; ++j) {
                                 const int i = 16 * k + 4 * j;
                                 const int v = i < 24 ? i : i < 168 ? i - 24 : i < 176 ? i - 144 : i < 288 ? i - 32 : i - 288;
-                                w4[j] = (uint32_t)v * 0x01010101u + 0x03020100u;
+                                *lw(T, 4 * k + j) = (uint32_t)v * 0x01010101u + 0x03020100u;
                             }
-                            dst4[k] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
                         }
-                        LE[7] = 0;
-                        LE[8] = 168;
-                        LE[9] = 288;
+                        // litend: LE[7] = 0, LE[8] = 168, LE[9] = 288
+                        *lw(T, W_LE + 3) = 0u << 16;
+                        *lw(T, W_LE + 4) = 168u | (288u << 16);
                         // make_canon of the fixed counts (7: 24, 8: 152, 9: 112; distances 5: 32)
                         constexpr uint32_t kFixL[15] = {0x00000800u, 0x00001000u, 0x00001800u, 0x00002000u,
                                                         0x00002800u, 0x00003000u, 0x0c003818u, 0x320040b0u,
@@ -1246,14 +1291,12 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
                             const uint32_t l = (uint32_t)(clp >> (3 * i)) & 7u;
                             const uint32_t at = (uint32_t)(offs >> (5 * l)) & 31u;
                             offs += 1ull << (5 * l);
-                            if (l) T[O_CLS + at] = (uint8_t)i;
+                            if (l) *lb(T, O_CLS + at) = (uint8_t)i;
                         }
-                        uint64_t* nib = (uint64_t*)(T + O_NIB);
 #pragma unroll
-                        for (int k = 0; k < 20; ++k) nib[k] = 0;
-                        uint4* h4 = (uint4*)H;
+                        for (int k = 0; k < 40; ++k) *lw(T, W_NIB + k) = 0u;
 #pragma unroll
-                        for (int k = 0; k < 4; ++k) h4[k] = make_uint4(0, 0, 0, 0);
+                        for (int k = 0; k < 16; ++k) *lw(T, W_HIST + k) = 0u;
                         want = nlen + ndist;
                         have = 0;
                         prev = 0;
@@ -1274,7 +1317,7 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
                     const uint32_t c7 = __builtin_bitreverse32((uint32_t)bb) >> 25;
                     const Sym yc = canon_decode<7>(tc.Q, c7);
                     L = yc.L;
-                    csym = T[O_CLS + (yc.idx < 19 ? yc.idx : 0u)];
+                    csym = *lb(T, O_CLS + (yc.idx < 19 ? yc.idx : 0u));
                 }
                 if (avail < (int32_t)tc.root) {
                     st = S_DONE;
@@ -1314,10 +1357,10 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
                             const uint32_t a = have, b = have + rep;
                             const uint64_t pat = ((uint64_t)val * 0x1111111111111111ull) & ((1ull << (4 * rep)) - 1);
                             const uint64_t v = pat << ((a & 7) * 4);
-                            uint32_t* nw = (uint32_t*)(T + O_NIB) + (a >> 3);
-                            __hip_atomic_fetch_or(nw, (uint32_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            __hip_atomic_fetch_or(lw(T, W_NIB + (a >> 3)), (uint32_t)v, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
                             if ((uint32_t)(v >> 32))
-                                __hip_atomic_fetch_or(nw + 1, (uint32_t)(v >> 32), __ATOMIC_RELAXED,
+                                __hip_atomic_fetch_or(lw(T, W_NIB + (a >> 3) + 1), (uint32_t)(v >> 32), __ATOMIC_RELAXED,
                                                       __HIP_MEMORY_SCOPE_WORKGROUP);
                             const uint32_t e_l = b < nlen ? b : nlen;
                             const uint32_t nl = e_l > a ? e_l - a : 0u;
@@ -1325,7 +1368,7 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
                             const uint32_t nlo = e_o > a ? e_o - a : 0u;
                             const uint32_t s_d = a > nlen ? a : nlen;
                             const uint32_t nd = b > s_d ? b - s_d : 0u;
-                            __hip_atomic_fetch_add(H + val, nl | (nlo << 10) | (nd << 20), __ATOMIC_RELAXED,
+                            __hip_atomic_fetch_add(lw(T, W_HIST + val), nl | (nlo << 10) | (nd << 20), __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_WORKGROUP);
                             if (a <= 256 && 256 < b) eob_seen = true;
                         }
@@ -1341,15 +1384,8 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
                 st = S_DONE;
             } else {
                 uint32_t h[16];
-                const uint4* h4 = (const uint4*)H;
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint4 v = h4[k];
-                    h[4 * k] = v.x;
-                    h[4 * k + 1] = v.y;
-                    h[4 * k + 2] = v.z;
-                    h[4 * k + 3] = v.w;
-                }
+                for (int k = 0; k < 16; ++k) h[k] = *lw(T, W_HIST + k);
                 uint32_t c[16];
                 c[0] = 0;
 #pragma unroll
@@ -1371,14 +1407,14 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
                     for (int l = 0; l < 16; l += 2) {
                         const uint32_t a0 = l ? h[l] : 0u, a1 = h[l + 1];
                         const uint32_t le0 = cl_ + ((a0 >> 10) & 0x3ffu);
-                        H[l] = cl_ | (cd_ << 16);
+                        *lw(T, W_HIST + l) = cl_ | (cd_ << 16);
                         cl_ += a0 & 0x3ffu;
                         cd_ += (a0 >> 20) & 0x3ffu;
                         const uint32_t le1 = cl_ + ((a1 >> 10) & 0x3ffu);
-                        H[l + 1] = cl_ | (cd_ << 16);
+                        *lw(T, W_HIST + l + 1) = cl_ | (cd_ << 16);
                         cl_ += a1 & 0x3ffu;
                         cd_ += (a1 >> 20) & 0x3ffu;
-                        ((uint32_t*)LE)[l >> 1] = le0 | (le1 << 16);
+                        *lw(T, W_LE + (l >> 1)) = le0 | (le1 << 16);
                     }
                     have = 0;
                     st = S_PASS2;
@@ -1389,7 +1425,7 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
             // place symbols in canonical order (inflate_stream.ipp:632-640)
 #pragma unroll
             for (uint32_t h8 = 0; h8 < KNIB; h8 += 8) {
-                const uint32_t w = ((const uint32_t*)(T + O_NIB))[(have + h8) >> 3];
+                const uint32_t w = *lw(T, W_NIB + ((have + h8) >> 3));
                 uint32_t olds[8];
                 // all fetch-adds first (no branch between them), then the
                 // placements: one LDS round trip for the eight
@@ -1398,15 +1434,15 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
                     const uint32_t i = have + h8 + k;
                     const uint32_t l = (w >> (4 * k)) & 15u;
                     const uint32_t inc = (l && i < want) ? (i < nlen ? 1u : 0x10000u) : 0u;
-                    olds[k] = __hip_atomic_fetch_add(H + l, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    olds[k] = __hip_atomic_fetch_add(lw(T, W_HIST + l), inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
 #pragma unroll
                 for (uint32_t k = 0; k < 8; ++k) {
                     const uint32_t i = have + h8 + k;
                     const uint32_t l = (w >> (4 * k)) & 15u;
                     if (l && i < want) {
-                        if (i < nlen) T[O_LIT + (olds[k] & 0xffffu)] = (uint8_t)i;
-                        else T[O_DST + (olds[k] >> 16)] = (uint8_t)(i - nlen);
+                        if (i < nlen) *lb(T, O_LIT + (olds[k] & 0xffffu)) = (uint8_t)i;
+                        else *lb(T, O_DST + (olds[k] >> 16)) = (uint8_t)(i - nlen);
                     }
                 }
             }
@@ -1428,10 +1464,10 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
                               : data ? make_uint2(elit, estored ? (TOK_STORED | estored)
                                                                 : (enl | (emlen << 3) | (edist << 12)))
                                      : make_uint2(pos, TOK_END | hand | ((uint32_t)result & 0xffu));
-            if (adv) *(uint2*)(T + ring_at(head)) = ent;
+            if (adv) ring_st(T, head, ent);
             compiler_fence();
             head += adv ? 1u : 0u;
-            lds_store(T + O_HEAD, head);
+            lds_store((uint8_t*)lw(T, W_HEAD), head);
             fin = fin || (adv && endt);
             if (adv && ctl) {
                 if (send_new) begin(msg);
@@ -1454,10 +1490,10 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
             if (st0 == S_DATA && st == S_DATA && !nx_used && head - taken < RING)
                 data_step(enl2, elit2, emlen2, edist2);
             const bool adv2 = enl2 != 0 || emlen2 != 0;
-            if (adv2) *(uint2*)(T + ring_at(head)) = make_uint2(elit2, enl2 | (emlen2 << 3) | (edist2 << 12));
+            if (adv2) ring_st(T, head, make_uint2(elit2, enl2 | (emlen2 << 3) | (edist2 << 12)));
             compiler_fence();
             head += adv2 ? 1u : 0u;
-            lds_store(T + O_HEAD, head);
+            lds_store((uint8_t*)lw(T, W_HEAD), head);
         }
         // blocked on a full ring in every lane: leave the SIMD to the expander
         if (!__ballot(head != head0 || st != st0 || (st != S_DATA && st != S_SCOPY && st != S_DONE))) {
@@ -1492,7 +1528,7 @@ inflate_lane3_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict_
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const unsigned lane = threadIdx.x & 63u;
     const bool is_decoder = threadIdx.x < 64;
-    uint8_t* T = smem + lane * STRIDE;
+    uint8_t* T = lane_area(smem, lane);
     // skip: the first *skip entries of `order` belong to the wave kernel (the
     // long payloads of a work-queue batch, pmd_capi.hip inflate_impl)
     const uint32_t s0 = skip ? *skip : 0u;
@@ -1503,7 +1539,10 @@ inflate_lane3_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict_
     // max_in != 0: only payloads of at most max_in bytes (the rest go to the
     // wave kernel, see inflate_impl in pmd_capi.hip)
     if (valid && max_in && in_len[m] > max_in) valid = false;
-    if (is_decoder) *(uint2*)(T + O_HEAD) = make_uint2(0, 0);
+    if (is_decoder) {
+        *lw(T, W_HEAD) = 0u;
+        *lw(T, W_TAIL) = 0u;
+    }
     __syncthreads();
     if (is_decoder) {
         if (BPMD3_DPRIO) __builtin_amdgcn_s_setprio(BPMD3_DPRIO);   // the decoder sets the pace
@@ -1528,10 +1567,13 @@ inflate_lane3_seg_kernel(const uint8_t* __restrict__ in, const uint64_t* __restr
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const unsigned lane = threadIdx.x & 63u;
     const bool is_decoder = threadIdx.x < 64;
-    uint8_t* T = smem + lane * STRIDE;
+    uint8_t* T = lane_area(smem, lane);
     const uint32_t j = blockIdx.x * WG_MSGS + lane;
     const bool valid = j < n_tasks;
-    if (is_decoder) *(uint2*)(T + O_HEAD) = make_uint2(0, 0);
+    if (is_decoder) {
+        *lw(T, W_HEAD) = 0u;
+        *lw(T, W_TAIL) = 0u;
+    }
     __syncthreads();
     if (is_decoder) {
         if (BPMD3_DPRIO) __builtin_amdgcn_s_setprio(BPMD3_DPRIO);

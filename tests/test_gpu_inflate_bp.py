@@ -280,15 +280,15 @@ def test_reserved_too_small_spills_then_grows():
     """A reserve far below the batch: the fitting prefix decodes
     block-parallel, the rest through the wave kernel, all exact; the next
     call has grown to the batch and spills nothing."""
-    src, comp, cap = _c5_like(512, 0x5EED0062)
+    src, comp, cap = _c5_like(2048, 0x5EED0062)   # >= 2048: the lane/bp path, not the wave kernel
     pmd = _pmd()
 
     def body(st):
         pmd.inflate_reserve(65536, 65536, 1, stream=st)
         ok, c = _call(st, comp, cap, src)
-        assert ok and c[3] > 0 and c[0] + c[3] == 512, c[:4]
+        assert ok and c[3] > 0 and c[0] + c[3] == 2048, c[:4]
         ok, c = _call(st, comp, cap, src)
-        assert ok and c[0] == 512 and c[2] == 0 and c[3] == 0, c[:4]
+        assert ok and c[0] == 2048 and c[2] == 0 and c[3] == 0, c[:4]
     _on_fresh_stream(body)
 
 
@@ -297,7 +297,7 @@ def test_failed_workspace_allocation_falls_back():
     smaller workspace (exact output, spills to the wave kernel), and the next
     call on the same stream grows it again and decodes everything
     block-parallel."""
-    src, comp, cap = _c5_like(512, 0x5EED0063)
+    src, comp, cap = _c5_like(2048, 0x5EED0063)
     pmd = _pmd()
 
     def body(st):
@@ -308,5 +308,5 @@ def test_failed_workspace_allocation_falls_back():
             pmd.lib().bpmd_diag_bp_fail_alloc(0)
         assert ok and c[3] > 0, c[:4]
         ok, c = _call(st, comp, cap, src)
-        assert ok and c[0] == 512 and c[3] == 0, c[:4]
+        assert ok and c[0] == 2048 and c[3] == 0, c[:4]
     _on_fresh_stream(body)
