@@ -74,6 +74,32 @@ def pmd_compress_host(data, off, lens, level=6, wbits=15, mem=4):
     return out
 
 
+def beast_payloads(raw, off, lens, level, mem=4, wbits=15, threads=None):
+    """pmd_compress_host over a whole batch on the host's cores: CPython's
+    zlib (byte-identical to Beast's deflate_stream at these settings,
+    tests/test_oracle.py) releases the GIL while it compresses, so a thread
+    pool scales.  These are the payloads a Beast peer sends: blocks every
+    lit_bufsize - 1 symbols (deflate_stream.ipp:1406), stored / fixed /
+    dynamic as tr_flush_block picks, no sync markers inside a message."""
+    from concurrent.futures import ThreadPoolExecutor
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = threads or max(1, min(16, cores))
+    mv = memoryview(raw)
+    n = len(lens)
+    step = max(1, min(4096, n // (4 * threads) or 1))
+
+    def chunk(a):
+        out = []
+        for i in range(a, min(n, a + step)):
+            o, k = int(off[i]), int(lens[i])
+            c = zlib.compressobj(level, zlib.DEFLATED, -wbits, mem)
+            out.append((c.compress(mv[o:o + k]) + c.flush(zlib.Z_BLOCK) + c.flush(zlib.Z_SYNC_FLUSH))[:-4])
+        return out
+
+    with ThreadPoolExecutor(threads) as ex:
+        return [p for part in ex.map(chunk, range(0, n, step)) for p in part], threads
+
+
 def pack(payloads, align=16):
     lens = np.fromiter((len(p) for p in payloads), dtype=np.int64, count=len(payloads))
     slot = (lens + align - 1) // align * align
@@ -344,6 +370,7 @@ def mixed_legs(args, rank, world, timer, dev):
     if args.legs:
         legs = [l for l in legs if l[0] in args.legs.split(",")]
     batches = {}
+    host = {}
     for name, kind, lens_all, seed, level in legs:
         s0, e0, per_rank = shard_config(lens_all, rank, world)
         lens = lens_all[s0:e0]
@@ -352,6 +379,7 @@ def mixed_legs(args, rank, world, timer, dev):
             raw, off, ln = synth.make_batch(kind, lens, seed=seed, first=s0)
             batches = {key: pmd.Batch(torch.from_numpy(raw).to(dev), torch.from_numpy(off.astype(np.int64)).to(dev),
                                       torch.from_numpy(ln.astype(np.int32)).to(dev))}
+            host = {key: (raw, off, ln)} if not args.no_beast_payloads else {}
             del raw
         src = batches[key]
         total = int(lens.astype(np.int64).sum())
@@ -393,14 +421,49 @@ def mixed_legs(args, rank, world, timer, dev):
                      "inflate_roofline": roofline(alg, i_kern, INFLATE_STEP_KERNELS[name],
                                                   pmc_traffic_leg(name, "inflate")),
                      "ratio_rank_local": round(comp_bytes / max(1, total), 4), "roundtrip_ok": bool(ok)}
+        # the same messages as a Beast peer deflates them (host zlib, this
+        # leg's level, memLevel 4): the inflate rate on payloads without this
+        # library's sync markers (VERDICT r4 "what's weak" 2)
+        bstep = None
+        if key in host:
+            hraw, hoff, hln = host[key]
+            t0 = time.perf_counter()
+            bp_list, thr = beast_payloads(hraw, hoff, hln, level)
+            t_comp = time.perf_counter() - t0
+            bbuf, boff, blen = pack(bp_list)
+            del bp_list
+            bsrc = pmd.Batch(torch.from_numpy(bbuf).to(dev), torch.from_numpy(boff).to(dev),
+                             torch.from_numpy(blen).to(dev))
+            bcomp = int(blen.astype(np.int64).sum())
+            del bbuf
+
+            def beast_step(a=0, b=len(lens)):
+                sub = bsrc if (a, b) == (0, len(lens)) else pmd.Batch(bsrc.data, bsrc.off[a:b], bsrc.len[a:b])
+                return pmd.inflate_batch(sub, src.len[a:b], out=rbuf, out_off=src.off[a:b])
+
+            rb = beast_step()
+            torch.cuda.synchronize()
+            okb = (int((rb.status != 0).sum()) == 0 and torch.equal(rb.out.len, src.len)
+                   and torch.equal(rbuf[:total], src.data[:total]))
+            if not okb:
+                log(f"[rank {rank}] {name} BEAST-PAYLOAD INFLATE FAILURE")
+            bstep, b_kern = timer.run(beast_step, steps, 1)
+            out[name].update({
+                "inflate_beast_value": round(total_all / (1 << 30) / bstep, 3),
+                "inflate_beast_roofline": roofline(total + bcomp + 16 * len(lens), b_kern, INFLATE_STEP_KERNELS[name]),
+                "inflate_beast_ok": bool(okb), "beast_ratio_rank_local": round(bcomp / max(1, total), 4),
+                "beast_payloads": f"host zlib (= Beast deflate_stream) L{level}/mem4/w15 + pmd framing, "
+                                  f"{thr} threads, {t_comp:.1f} s"})
         if world == 1 and not args.no_virtual_shards:
             from beast_amd import shard
             vs = {}
             for parts in (2, 4, 8):
-                dt, it = [], []
+                dt, it, bt = [], [], []
                 for a, b in shard.byte_balanced_ranges(lens, parts):
                     dt.append(timer.run(lambda: deflate_step(a, b), steps, 1)[0])
                     it.append(timer.run(lambda: inflate_step(a, b), steps, 1)[0])
+                    if bstep is not None:
+                        bt.append(timer.run(lambda: beast_step(a, b), steps, 1)[0])
                 vs[str(parts)] = {
                     "deflate_shard_ms": [round(t * 1e3, 3) for t in dt],
                     "inflate_shard_ms": [round(t * 1e3, 3) for t in it],
@@ -408,7 +471,14 @@ def mixed_legs(args, rank, world, timer, dev):
                     "inflate_projected_value": round(total / (1 << 30) / max(it), 3),
                     "deflate_projected_speedup": round(d_step / max(dt), 3),
                     "inflate_projected_speedup": round(i_step / max(it), 3)}
+                if bt:
+                    vs[str(parts)].update({
+                        "inflate_beast_shard_ms": [round(t * 1e3, 3) for t in bt],
+                        "inflate_beast_projected_value": round(total / (1 << 30) / max(bt), 3),
+                        "inflate_beast_projected_speedup": round(bstep / max(bt), 3)})
             out[name]["virtual_shards"] = vs
+        if bstep is not None:
+            del bsrc, rb
         del cbuf, rbuf, comp, d, r
     return out
 
@@ -458,6 +528,8 @@ def main():
     ap.add_argument("--no-frame", action="store_true")
     ap.add_argument("--no-mixed", action="store_true")
     ap.add_argument("--legs", default="", help="comma list of mixed legs to run (c4_l6,c5_l1,c5_l6); default all")
+    ap.add_argument("--no-beast-payloads", action="store_true",
+                    help="skip the mixed legs' inflate of Beast-produced (host zlib) payloads")
     ap.add_argument("--no-virtual-shards", action="store_true",
                     help="skip the N=1 per-shard timing that projects the 2/4/8-GPU aggregate")
     ap.add_argument("--c4-msgs", type=int, default=C4_MSGS, help="configs[3] batch (all ranks together)")
