@@ -908,6 +908,253 @@ bp_resolve_kernel(const uint32_t* __restrict__ order, const uint32_t* __restrict
     }
 }
 
+// ------------------------------------------------- segment-parallel resolve
+// Round 4's resolve walked each payload's segments in order on one wave,
+// because a reference reads bytes the earlier segments write: a 64 KiB
+// payload was 64 dependent steps, and the longest payloads set the kernel's
+// end.  Now two kernels, the phase boundary between them a kernel boundary
+// (no workgroup ever waits for another):
+//   bp_chain_kernel   one lane per payload walks the chain of segment
+//                     results only (no symbols): each on-chain segment's
+//                     output start and slot, the capacity cut, the status,
+//                     the fallbacks;
+//   bp_resolve2_kernel one workgroup per payload (a queue over payloads)
+//                     resolves all its segments at once: a reference is
+//                     followed into the SYMBOLS of the segment that holds its
+//                     target (found by a binary search over the chain's
+//                     output starts in LDS) and on, while the target is itself
+//                     a reference -- symbols never change after decoding, so
+//                     no order between segments is needed.  The first
+//                     reference before the payload's start (the reference's
+//                     invalid_distance, inflate_stream.ipp:475-514) is found
+//                     in a first pass, so no byte at or past it is written.
+struct PayRes {
+    uint32_t nseg;     // segments on the chain up to the terminating one
+    uint32_t olen;     // output length by the chain alone (capacity / status)
+    int32_t status;    // status by the chain alone
+    uint32_t flags;    // 1 fallback (wave kernel), 2 capacity cut
+};
+static_assert(sizeof(PayRes) == 16, "PayRes layout");
+
+__global__ void __launch_bounds__(256)
+bp_chain_kernel(const uint32_t* __restrict__ order, const uint32_t* __restrict__ nlong,
+                const uint32_t* __restrict__ task_base, const SegTask* __restrict__ tasks,
+                const SegRes* __restrict__ res, const uint32_t* __restrict__ out_cap, uint32_t raw,
+                const Stat* __restrict__ stats, uint32_t* __restrict__ chp, uint64_t* __restrict__ chs,
+                PayRes* __restrict__ pay, uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
+                uint32_t* __restrict__ fb_list, uint32_t* __restrict__ fb_count)
+{
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= *nlong) return;
+    const uint32_t m = order[i];
+    const uint32_t cap = out_cap[m];
+    const uint32_t tb = task_base[i];
+    const int32_t full_status = raw ? ST_OK : ST_NEED_BUFFERS;
+    PayRes pr = {0, 0, ST_OK, 0};
+    if (stats[i].regions == 0) {
+        pr.flags = 1;
+    } else {
+        uint32_t t = tb, P = 0, k = 0;
+        for (;;) {
+            const SegRes r = res[t];
+            chp[tb + k] = P;
+            chs[tb + k] = tasks[t].sym_off;
+            ++k;
+            if (r.nsym > cap - P) {   // the capacity cuts this segment
+                pr.status = full_status;
+                pr.olen = cap;
+                pr.flags = 2;
+                break;
+            }
+            P += r.nsym;
+            if (r.status == SEG_HANDOFF && r.next > t && r.next != 0xffffffffu) {
+                t = r.next;
+                continue;
+            }
+            if (r.status == SEG_FULL || r.status == SEG_SKIP || r.status == SEG_HANDOFF) {
+                pr.flags = 1;
+                {
+                    g_bp_fb[0] = m;
+                    g_bp_fb[1] = t - tb;
+                    g_bp_fb[2] = (uint32_t)r.status;
+                    g_bp_fb[3] = r.nsym;
+                    g_bp_fb[4] = tasks[t].sym_cap;
+                    g_bp_fb[5] = r.next;
+                    g_bp_fb[6] = tasks[t].bit;
+                    g_bp_fb[7] = tasks[t].kind;
+                }
+                break;
+            }
+            pr.status = r.status;
+            pr.olen = P;
+            break;
+        }
+        pr.nseg = k;
+        atomicAdd(&g_bp_diag[1], (unsigned long long)k);
+    }
+    atomicAdd(&g_bp_diag[0], 1ull);
+    if (pr.flags & 1) {
+        atomicAdd(&g_bp_diag[2], 1ull);
+        fb_list[atomicAdd(fb_count, 1u)] = m;
+    }
+    pay[i] = pr;
+    (void)out_len;
+    (void)status;
+}
+
+constexpr uint32_t RES_THREADS = 256;
+constexpr uint32_t RES_LDS_SEGS = 1024;   // chains up to this length resolve from LDS
+constexpr uint32_t RES_HOPS = 32;         // references followed per byte in pass 2
+
+// the chain segment holding output position q (chp ascending, chp[0] = 0)
+__device__ __forceinline__ uint32_t seg_of(const uint32_t* __restrict__ P, uint32_t K, uint32_t q)
+{
+    uint32_t lo = 0, hi = K - 1;   // largest k with P[k] <= q
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (P[mid] <= q) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(RES_THREADS)
+bp_resolve2_kernel(const uint32_t* __restrict__ order, const uint32_t* __restrict__ nlong,
+                   const uint32_t* __restrict__ task_base, const uint16_t* __restrict__ sym,
+                   uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
+                   const uint32_t* __restrict__ out_cap, uint32_t* __restrict__ out_len,
+                   int32_t* __restrict__ status, uint32_t raw, const uint32_t* __restrict__ chp,
+                   const uint64_t* __restrict__ chs, const PayRes* __restrict__ pay, uint32_t* __restrict__ qctr)
+{
+    __shared__ uint32_t sP[RES_LDS_SEGS];
+    __shared__ uint64_t sS[RES_LDS_SEGS];
+    __shared__ uint32_t s_i, s_bad, s_deep;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t end = *nlong;
+    for (;;) {
+        if (tid == 0) s_i = atomicAdd(qctr, 1u);
+        __syncthreads();
+        const uint32_t i = s_i;
+        if (i >= end) break;
+        const PayRes pr = pay[i];
+        if (pr.flags & 1) {   // the wave kernel decodes it (bp_chain_kernel listed it)
+            __syncthreads();
+            continue;
+        }
+        const uint32_t m = order[i];
+        const uint32_t cap = out_cap[m];
+        uint8_t* o = out + out_off[m];
+        const uint32_t tb = task_base[i];
+        const uint32_t K = pr.nseg;
+        const bool lds = K <= RES_LDS_SEGS;
+        for (uint32_t k = tid; k < K && lds; k += RES_THREADS) {
+            sP[k] = chp[tb + k];
+            sS[k] = chs[tb + k];
+        }
+        if (tid == 0) {
+            s_bad = 0xffffffffu;
+            s_deep = 0;
+        }
+        __syncthreads();
+        const uint32_t* P = lds ? sP : chp + tb;
+        const uint64_t* S = lds ? sS : chs + tb;
+        // positions whose references count: the output, plus (pmd mode) the
+        // token at the capacity when the capacity cut the chain -- a bad
+        // distance there is the reference's error, not need_buffers
+        const uint32_t lim = pr.olen + ((pr.flags & 2) && !raw ? 1u : 0u);
+        // pass 1: the first reference before the payload's start
+        for (uint32_t k = 0; k < K; ++k) {
+            const uint32_t p0 = P[k], p1 = k + 1 < K ? P[k + 1] : lim;
+            const uint32_t n = p1 > p0 ? p1 - p0 : 0u;
+            const uint16_t* sy = sym + S[k];
+            for (uint32_t j = tid * 4; j < n; j += RES_THREADS * 4) {
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q) {
+                    if (j + q < n) {
+                        const uint32_t v = sy[j + q];
+                        if ((v & SYM_REF) && (v & 0x7fffu) + 1 > p0) atomicMin(&s_bad, p0 + j + q);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        const uint32_t bad = s_bad;
+        const uint32_t olen = bad < lim ? bad : pr.olen;
+        // pass 2: bytes [0, olen), 4 per thread per step; a reference is
+        // followed through the symbols until a literal, at most RES_HOPS
+        // times (a run of one byte repeated across many segments -- a
+        // distance-1 match carried from segment to segment -- would take one
+        // hop per segment for every byte: such a payload is finished by
+        // pass 3 instead)
+        bool deep = false;
+        for (uint32_t k = 0; k < K; ++k) {
+            const uint32_t p0 = P[k];
+            if (p0 >= olen) break;
+            const uint32_t p1 = k + 1 < K ? (P[k + 1] < olen ? P[k + 1] : olen) : olen;
+            const uint16_t* sy = sym + S[k];
+            for (uint32_t j = tid * 4; p0 + j < p1; j += RES_THREADS * 4) {
+                uint32_t b[4];
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q) {
+                    b[q] = 0;
+                    if (p0 + j + q < p1) {
+                        uint32_t v = sy[j + q];
+                        uint32_t base = p0;   // output start of the segment v belongs to
+                        for (uint32_t h = 0; (v & SYM_REF) && h < RES_HOPS; ++h) {
+                            const uint32_t t = base - ((v & 0x7fffu) + 1);   // >= 0 before `bad`
+                            const uint32_t kk = seg_of(P, K, t);
+                            base = P[kk];
+                            v = sym[S[kk] + (t - base)];
+                        }
+                        deep = deep || (v & SYM_REF);
+                        b[q] = v & 0xffu;
+                    }
+                }
+                const uint32_t x = p0 + j;
+                if (x + 4 <= p1) {
+                    *(uint32_ua*)(o + x) = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
+                } else {
+#pragma unroll
+                    for (uint32_t q = 0; q < 4; ++q)
+                        if (x + q < p1) o[x + q] = (uint8_t)b[q];
+                }
+            }
+        }
+        if (deep) s_deep = 1;
+        __syncthreads();
+        if (s_deep) {
+            // pass 3: segment by segment in stream order, a reference reading
+            // the byte the earlier segments wrote (round 4's resolve, with the
+            // workgroup's four waves on each segment; the barrier makes the
+            // bytes visible across them)
+            for (uint32_t k = 0; k < K; ++k) {
+                const uint32_t p0 = P[k];
+                if (p0 >= olen) break;
+                const uint32_t p1 = k + 1 < K ? (P[k + 1] < olen ? P[k + 1] : olen) : olen;
+                const uint16_t* sy = sym + S[k];
+                for (uint32_t j = tid * 4; p0 + j < p1; j += RES_THREADS * 4) {
+#pragma unroll
+                    for (uint32_t q = 0; q < 4; ++q) {
+                        if (p0 + j + q < p1) {
+                            const uint32_t v = sy[j + q];
+                            o[p0 + j + q] = (v & SYM_REF) ? o[p0 - ((v & 0x7fffu) + 1)] : (uint8_t)v;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        if (tid == 0) {
+            const bool inval = bad < lim;
+            out_len[m] = olen;
+            // (bad < lim: before the capacity in raw mode, at or before it in
+            // pmd mode -- the serial decoder's order of the two checks)
+            status[m] = inval ? ST_INVALID_DISTANCE : pr.status;
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace bp
 }  // namespace bpmd
 
@@ -963,14 +1210,31 @@ BpCaps* caps_for(int dev, hipStream_t s)
     return &g_bp_caps.back();
 }
 
-// decode workspace bytes for a capacity (n: the batch's message count)
+// decode workspace layout for a capacity (n: the batch's message count):
+// tasks, results, fallback list, region map, marks, the resolve's chains
+// (output start and slot of every segment on a payload's chain, in chain
+// order at the payload's first task; per payload: chain length, output
+// length, status), symbols
+struct DwLayout {
+    size_t tasks, res, fb, map, mark, chp, chs, pay, sym, bytes;
+    DwLayout(unsigned long long nt, unsigned long long words, uint32_t n)
+    {
+        using namespace bpmd::bp;
+        tasks = 0;
+        res = al256(tasks + sizeof(SegTask) * nt);
+        fb = al256(res + sizeof(SegRes) * nt);
+        map = al256(fb + 4ull * n);
+        mark = al256(map + 4ull * nt);
+        chp = al256(mark + 4ull * n);
+        chs = al256(chp + 4ull * nt);
+        pay = al256(chs + 8ull * nt);
+        sym = al256(pay + sizeof(PayRes) * (size_t)n);
+        bytes = al256(sym + 2ull * (words + SYM_GUARD + 64));
+    }
+};
 inline size_t dw_bytes(unsigned long long tasks, unsigned long long words, uint32_t n)
 {
-    using namespace bpmd::bp;
-    const size_t d_res = al256(sizeof(SegTask) * tasks), d_fb = al256(d_res + sizeof(SegRes) * tasks),
-                 d_map = al256(d_fb + 4ull * n), d_mark = al256(d_map + 4ull * tasks),
-                 d_sym = al256(d_mark + 4ull * n);
-    return al256(d_sym + 2ull * (words + SYM_GUARD + 64));
+    return DwLayout(tasks, words, n).bytes;
 }
 
 // a capacity of t tasks and w words plus a quarter, within half the free memory
@@ -1147,15 +1411,16 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
             c->words = cap_words;
         }
     }
-    const size_t d_tasks = 0, d_res = al256(d_tasks + sizeof(SegTask) * cap_tasks),
-                 d_fb = al256(d_res + sizeof(SegRes) * cap_tasks), d_map = al256(d_fb + 4ull * n),
-                 d_mark = al256(d_map + 4ull * cap_tasks), d_sym = al256(d_mark + 4ull * n);
-    SegTask* tasks = (SegTask*)(dw + d_tasks);
-    SegRes* res = (SegRes*)(dw + d_res);
-    uint32_t* fb = (uint32_t*)(dw + d_fb);
-    uint16_t* sym = (uint16_t*)(dw + d_sym);
-    uint32_t* rmap = (uint32_t*)(dw + d_map);
-    uint32_t* marked = (uint32_t*)(dw + d_mark);
+    const DwLayout D(cap_tasks, cap_words, n);
+    SegTask* tasks = (SegTask*)(dw + D.tasks);
+    SegRes* res = (SegRes*)(dw + D.res);
+    uint32_t* fb = (uint32_t*)(dw + D.fb);
+    uint16_t* sym = (uint16_t*)(dw + D.sym);
+    uint32_t* rmap = (uint32_t*)(dw + D.map);
+    uint32_t* marked = (uint32_t*)(dw + D.mark);
+    uint32_t* chp = (uint32_t*)(dw + D.chp);
+    uint64_t* chs = (uint64_t*)(dw + D.chs);
+    PayRes* pay = (PayRes*)(dw + D.pay);
     if (hipMemsetAsync(marked, 0, 4ull * n, s) != hipSuccess) return (int)hipErrorUnknown;
     hipLaunchKernelGGL(bp_fit_kernel, dim3(1), dim3(256), 0, s, nlong, reg, tbase, words, wbase, n, cap_tasks,
                        cap_words, order, fit, dtot, fb, q + 2);
@@ -1186,9 +1451,24 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
     int e = bpmd_internal_inflate_lane3_seg(in, in_off, in_len, (uint32_t)cap_tasks, tasks, sym, res, raw, q + 3, wgs,
                                             s, fit + 1);
     if (e) return e;
-    hipLaunchKernelGGL(bp_resolve_kernel, dim3(8u * cus), dim3(256), 0, s, order, fit, tbase, tasks, res,
-                       sym, out, out_off, out_cap, out_len, status, raw, fb, q + 2, q + 1, st);
-    if (hipGetLastError() != hipSuccess) return (int)hipErrorUnknown;
+    // resolve: segment-parallel (chain walk, then one workgroup per payload
+    // resolving every segment at once), or the serial walk of round 4
+    // (BPMD_BP_RESOLVE=serial, A/B only)
+    static const bool serial_resolve = [] {
+        const char* e = getenv("BPMD_BP_RESOLVE");
+        return e && !strcmp(e, "serial");
+    }();
+    if (serial_resolve) {
+        hipLaunchKernelGGL(bp_resolve_kernel, dim3(8u * cus), dim3(256), 0, s, order, fit, tbase, tasks, res,
+                           sym, out, out_off, out_cap, out_len, status, raw, fb, q + 2, q + 1, st);
+        if (hipGetLastError() != hipSuccess) return (int)hipErrorUnknown;
+    } else {
+        hipLaunchKernelGGL(bp_chain_kernel, dim3(n / 256 + 1), dim3(256), 0, s, order, fit, tbase, tasks, res, out_cap,
+                           raw, st, chp, chs, pay, out_len, status, fb, q + 2);
+        hipLaunchKernelGGL(bp_resolve2_kernel, dim3(8u * cus), dim3(RES_THREADS), 0, s, order, fit, tbase, sym, out,
+                           out_off, out_cap, out_len, status, raw, chp, chs, pay, q + 1);
+        if (hipGetLastError() != hipSuccess) return (int)hipErrorUnknown;
+    }
     // payloads over the capacity or whose output outgrew the slots: the wave
     // kernel, from the list
     return bpmd_internal_inflate_wave_ordered(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, raw,

@@ -1,8 +1,9 @@
 """End-to-end (PCIe-inclusive) rate: the path starts and ends in host memory
 (Boost.Asio socket buffers), so this times pinned host -> device copy,
 kernel, device -> host copy for the C2 inflate batch and the C3 deflate
-batch, pipelined in chunks over two HIP streams (copy of chunk i+1 overlaps
-the kernel of chunk i).  Reported in DESIGN.md; never the bench `value`.
+batch, pipelined in chunks over --depth HIP streams (H2D of chunk i+1, the kernel
+of chunk i and the D2H of chunk i-1 overlap; nothing in the loop waits on
+the device).  Reported in DESIGN.md; never the bench `value`.
 
     python scripts/e2e.py [--chunks 8] [--reps 5]
 """
@@ -34,14 +35,22 @@ def chunk_views(buf, off, lens, nchunks):
     return out
 
 
-def run_pipeline(chunks, kernel, out_bytes_of, reps):
+def run_pipeline(chunks, kernel, out_bytes_of, reps, depth=3):
+    """Chunk i runs on stream i % depth: its H2D, its batch call, its D2H of
+    the output and lengths.  Every device buffer is allocated up front (per
+    stream) and the batch calls get their output slots, so nothing in the
+    timed loop waits on the device: the H2D of chunk i + 1 and the D2H of
+    chunk i run on different streams, i.e. on the two copy directions at
+    once, beside the kernels."""
     dev = torch.device("cuda", 0)
-    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    streams = [torch.cuda.Stream() for _ in range(depth)]
     maxin = max(c[0].numel() for c in chunks)
     maxn = max(c[3] for c in chunks)
+    maxout = max(out_bytes_of(c[3]) for c in chunks)
     slots = [dict(d=torch.empty(maxin + 64, dtype=torch.uint8, device=dev),
                   o=torch.empty(maxn, dtype=torch.int64, device=dev),
-                  l=torch.empty(maxn, dtype=torch.int32, device=dev)) for _ in streams]
+                  l=torch.empty(maxn, dtype=torch.int32, device=dev),
+                  out=torch.empty(maxout + 64, dtype=torch.uint8, device=dev)) for _ in streams]
     outs_h = [torch.empty(out_bytes_of(c[3]), dtype=torch.uint8).pin_memory() for c in chunks]
     lens_h = [torch.empty(c[3], dtype=torch.int32).pin_memory() for c in chunks]
     times = []
@@ -49,14 +58,14 @@ def run_pipeline(chunks, kernel, out_bytes_of, reps):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i, (hd, ho, hl, n) in enumerate(chunks):
-            s = streams[i % 2]
-            sl = slots[i % 2]
+            s = streams[i % depth]
+            sl = slots[i % depth]
             with torch.cuda.stream(s):
                 sl["d"][: hd.numel()].copy_(hd, non_blocking=True)
                 sl["o"][:n].copy_(ho, non_blocking=True)
                 sl["l"][:n].copy_(hl, non_blocking=True)
                 src = pmd.Batch(sl["d"], sl["o"][:n], sl["l"][:n])
-                res = kernel(src, s)
+                res = kernel(src, s, sl["out"], n)
                 outs_h[i].copy_(res.out.data[: outs_h[i].numel()], non_blocking=True)
                 lens_h[i].copy_(res.out.len, non_blocking=True)
                 sl["keep"] = res
@@ -69,6 +78,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--chunks", type=int, default=8)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--depth", type=int, default=3, help="streams (chunks in flight)")
     ap.add_argument("--msgs", type=int, default=bench.N_MSGS)
     a = ap.parse_args()
     n, mb = a.msgs, bench.MSG_BYTES
@@ -79,7 +89,13 @@ def main():
     raw, roff, rlen = synth.make_batch("json", lens, seed=bench.SEED_C2)
     comp, coff, clen = bench.pack(bench.pmd_compress_host(raw, roff, rlen))
     chunks = chunk_views(comp, coff, clen, a.chunks)
-    t, outs, _ = run_pipeline(chunks, lambda src, s: pmd.inflate_batch(src, mb, stream=s), lambda k: k * mb, a.reps)
+    per = max(c[3] for c in chunks)
+    dev = torch.device("cuda", 0)
+    icap = torch.full((per,), mb, dtype=torch.int32, device=dev)
+    ioff = pmd.slot_offsets(icap)
+    t, outs, _ = run_pipeline(chunks, lambda src, s, out, k: pmd.inflate_batch(src, icap[:k], stream=s, out=out,
+                                                                             out_off=ioff[:k]),
+                              lambda k: k * mb, a.reps, a.depth)
     got = np.concatenate([o.numpy() for o in outs])
     res["inflate_e2e_GiBps"] = round(n * mb / (1 << 30) / t, 3)
     res["inflate_e2e_ok"] = bool(np.array_equal(got, raw[: n * mb]))
@@ -90,12 +106,26 @@ def main():
     ub = pmd.upper_bound(mb)
     slot = (ub + 15) // 16 * 16
     chunks3 = chunk_views(raw3, off3, len3, a.chunks)
-    t3, outs3, lens3 = run_pipeline(chunks3, lambda src, s: pmd.deflate_batch(src, level=6, stream=s),
-                                    lambda k: k * slot, a.reps)
+    dcap = torch.full((per,), ub, dtype=torch.int32, device=dev)
+    doff = pmd.slot_offsets(dcap)
+    t3, outs3, lens3 = run_pipeline(chunks3, lambda src, s, out, k: pmd.deflate_batch(src, level=6, stream=s,
+                                                                                     out_cap=dcap[:k], out=out,
+                                                                                     out_off=doff[:k]),
+                                    lambda k: k * slot, a.reps, a.depth)
+    rt = [pmd.Batch(torch.from_numpy(o.numpy()), doff[: len(l)].cpu(), l) for o, l in zip(outs3, lens3)]
+    ok3 = True
+    import zlib
+    for c, b in enumerate(rt[:1]):   # spot check: the first chunk's first 64 payloads inflate back (host zlib)
+        for j in range(64):
+            o, k = int(b.off[j]), int(b.len[j])
+            d = zlib.decompressobj(-15)
+            m = d.decompress(bytes(b.data[o:o + k].numpy()) + b"\x00\x00\xff\xff")
+            ok3 = ok3 and m == bytes(raw3[off3[j]:off3[j] + len3[j]])
+    res["deflate_e2e_spot_ok"] = bool(ok3)
     res["deflate_e2e_GiBps"] = round(n * mb / (1 << 30) / t3, 3)
     res["deflate_d2h_bytes"] = int(sum(int(x.numpy().sum()) for x in lens3))
     res["chunks"] = a.chunks
-    res["streams"] = 2
+    res["streams"] = a.depth
     print(json.dumps(res))
 
 

@@ -310,3 +310,27 @@ def test_failed_workspace_allocation_falls_back():
         ok, c = _call(st, comp, cap, src)
         assert ok and c[0] == 2048 and c[3] == 0, c[:4]
     _on_fresh_stream(body)
+
+
+def test_deep_reference_chains(mode):
+    """A 1 KiB pattern repeated with 5-10 % of its bytes changed each time:
+    most bytes copy the byte one period back, which was itself copied, so a
+    reference crosses many segments before it reaches a literal.  Chains
+    deeper than the resolve's hop limit are finished segment by segment
+    (pmd_inflate_bp.hip bp_resolve2_kernel pass 3); every byte must equal the
+    oracle's."""
+    rng = random.Random(0xDEE9)
+    payloads, caps = [], []
+    for size, rate in ((120000, 0.05), (65536, 0.10), (200000, 0.02)):
+        per = bytearray(rng.randbytes(1024))
+        data = bytearray()
+        while len(data) < size:
+            for _ in range(int(1024 * rate)):
+                per[rng.randrange(1024)] = rng.randrange(256)
+            data += per
+        data = bytes(data[:size])
+        for level, mem in ((6, 4), (1, 8)):
+            payloads.append(O.pmd_deflate(data, level, 15, mem))
+            caps.append(size)
+    _check(payloads, caps)
+    _check(payloads, caps, raw=True)
