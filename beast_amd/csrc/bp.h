@@ -27,6 +27,7 @@ constexpr int32_t SEG_SKIP = 102;      // no candidate in this region
 constexpr uint32_t KIND_START = 0;    // the payload's first bit
 constexpr uint32_t KIND_DYN = 1;      // a validated dynamic-block header (bit = its first bit)
 constexpr uint32_t KIND_STORED = 2;   // a validated stored block (bit = 8 x its LEN field's byte)
+constexpr uint32_t KIND_FIXED = 3;    // a fixed-code block reached by the skim (bit = its first bit)
 constexpr uint32_t KIND_NONE = 0xffu; // region without a candidate
 constexpr uint32_t KIND_PENDING = 0xfeu;  // scan pass 1: no stored block, the dynamic search pending
 

@@ -605,7 +605,9 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
                             const uint32_t w0 = peek32(S, lb), w1 = peek32(S, lb + 32), w2 = peek32(S, lb + 64),
                                            w3 = peek32(S, lb + 96);
                             const uint64_t lo = ((uint64_t)w1 << 32) | w0;
-                            uint64_t mk = ~(lo >> 1) & (lo >> 2);
+                            // BFINAL 0, BTYPE 2 (a final block is left to the
+                            // segment before it: halves the offsets to check)
+                            uint64_t mk = ~lo & ~(lo >> 1) & (lo >> 2);
                             mk &= ~((lo >> 4) & (lo >> 5) & (lo >> 6) & (lo >> 7));
                             mk &= ~((lo >> 9) & (lo >> 10) & (lo >> 11) & (lo >> 12));
                             uint32_t cand = (uint32_t)mk;
@@ -679,6 +681,216 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
         }
         __builtin_amdgcn_wave_barrier();
     }
+    }
+}
+
+// ------------------------------------------------------------------- skim
+// A Beast peer's long payloads carry no sync markers: tr_flush_block cuts a
+// block every lit_bufsize - 1 symbols and picks stored, fixed or dynamic by
+// size (deflate_stream.ipp:1406, :1425-1518), and near-random data gives
+// runs of stored and FIXED blocks.  A fixed block's header is three bits
+// that any bit offset can look like, so no scan finds it, and a run of them
+// was one serial segment.  The skim starts one lane at every candidate pass
+// 1 found (a stored block, or the payload's first bit) and walks the blocks
+// after it: a stored block by its LEN field, a fixed block symbol by symbol
+// with the fixed code (inflate_stream.ipp:865-930; no tables, no output),
+// until a dynamic block, the next candidate, a final block or an error.
+// Every block start it passes becomes its region's candidate when the region
+// has none (a dynamic block's start too), and the regions it crossed without
+// a block start are settled as candidate-free, so pass 2 searches only the
+// regions no walk reached.  A walk that meets anything unexpected simply
+// stops: candidates only ever cut the serial decode, which checks
+// everything again (bit-exact results do not depend on the skim).
+struct SkimBits {
+    const uint32_t* A;   // the payload's aligned base
+    uint32_t E;          // dwords holding payload bytes
+    uint32_t sbits;      // 8 x the payload's offset in A[0]
+    __device__ __forceinline__ uint32_t word(uint32_t w) const { return w < E ? A[w] : 0u; }
+};
+
+// the region of payload byte `byte` (bp_stats_kernel: na regions of R bytes,
+// the last one taking the rest)
+__device__ __forceinline__ uint32_t region_of(uint32_t byte, uint32_t R, uint32_t na)
+{
+    const uint32_t k = byte / R;
+    return k < na ? k : na - 1;
+}
+
+__global__ void __launch_bounds__(256)
+bp_skim_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+               const uint32_t* __restrict__ in_len, const uint32_t* __restrict__ order,
+               const uint32_t* __restrict__ region_map, const uint32_t* __restrict__ n_regions_dev,
+               const Stat* __restrict__ stats, const uint32_t* __restrict__ task_base, SegTask* __restrict__ tasks,
+               const uint32_t* __restrict__ marked)
+{
+    const uint32_t n_regions = *n_regions_dev;
+    for (uint32_t g = blockIdx.x * 256u + threadIdx.x; g < n_regions; g += gridDim.x * 256u) {
+    const SegTask t0 = tasks[g];
+    if (t0.kind != KIND_START && t0.kind != KIND_STORED) continue;
+    const uint32_t i = region_map[g];
+    if (marked[i]) continue;   // sync markers: pass 1 found the chunk starts
+    const Stat st = stats[i];
+    const uint32_t tb = task_base[i];
+    const uint32_t k0 = g - tb;
+    const uint32_t m = order[i];
+    const uint32_t len = in_len[m];
+    const uint8_t* p = in + in_off[m];
+    const uint32_t s = (uint32_t)((uintptr_t)p & 3u);
+    SkimBits B{(const uint32_t*)(p - s), (s + len + 3) >> 2, 8 * s};
+    // the next candidate pass 1 found (stored: its LEN field's bit)
+    uint32_t next_bit = 8 * len;
+    for (uint32_t k = k0 + 1; k < st.regions; ++k) {
+        const uint32_t kd = tasks[tb + k].kind;
+        if (kd == KIND_STORED) {
+            next_bit = tasks[tb + k].bit;
+            break;
+        }
+    }
+    const uint32_t end_bits = 8 * len;
+    // bit reader: 64 bits at `pos` from the dwords at w0 (+ the next one)
+    uint32_t pos;
+    bool stored_now;
+    if (t0.kind == KIND_STORED) {
+        pos = t0.bit;   // the LEN field
+        stored_now = true;
+    } else {
+        pos = 0;
+        stored_now = false;
+    }
+    uint32_t last_k = k0;   // the region of the last block start recorded (or the walk's own)
+    auto settle = [&](uint32_t kto) {   // regions after last_k up to kto (exclusive): no block start
+        for (uint32_t k = last_k + 1; k < kto && k < st.regions; ++k)
+            if (tasks[tb + k].kind == KIND_PENDING) tasks[tb + k].kind = KIND_NONE;
+    };
+    auto record = [&](uint32_t bit, uint32_t kind) {
+        const uint32_t k = region_of(bit >> 3, st.R, st.regions);
+        if (k <= last_k) return;   // a region that has its start already
+        settle(k);
+        SegTask& t = tasks[tb + k];
+        if (t.kind == KIND_PENDING || t.kind == KIND_NONE) {
+            t.bit = bit;
+            t.kind = kind;
+        }
+        last_k = k;
+    };
+    // bit reader: bb holds nb bits; refills take dwords from the 16-byte
+    // block q, and q is replaced by nx, which was loaded one block ahead, so
+    // a refill does not wait on memory once the walk is under way
+    uint4 q = make_uint4(0, 0, 0, 0), nx = q;
+    uint32_t qi = 0, bi = 0;   // dword index in q; block index of nx
+    uint64_t bb = 0;
+    uint32_t nb = 0;
+    auto load_block = [&](uint32_t b) -> uint4 {   // 16-byte block b of A, zeros past the payload
+        return 16 * b < 4 * B.E ? *(const uint4*)(B.A + 4 * b) : make_uint4(0, 0, 0, 0);
+    };
+    auto reset = [&](uint32_t at) {   // position the reader at payload bit `at`
+        const uint32_t qb = B.sbits + at;
+        const uint32_t blk = qb >> 7;
+        q = load_block(blk);
+        nx = load_block(blk + 1);
+        bi = blk + 1;
+        qi = (qb >> 5) & 3u;
+        const uint32_t d = qi == 0 ? q.x : qi == 1 ? q.y : qi == 2 ? q.z : q.w;
+        bb = (uint64_t)(d >> (qb & 31u));
+        nb = 32 - (qb & 31u);
+        ++qi;
+        pos = at;
+    };
+    auto fill = [&]() {
+        if (nb <= 32) {
+            if (qi == 4) {
+                q = nx;
+                nx = load_block(++bi);
+                qi = 0;
+            }
+            const uint32_t d = qi == 0 ? q.x : qi == 1 ? q.y : qi == 2 ? q.z : q.w;
+            bb |= (uint64_t)d << nb;
+            nb += 32;
+            ++qi;
+        }
+    };
+    auto take = [&](uint32_t n) {   // n <= 32 bits, after fill()
+        const uint32_t v = (uint32_t)bb & (n >= 32 ? ~0u : ((1u << n) - 1u));
+        bb >>= n;
+        nb -= n;
+        pos += n;
+        return v;
+    };
+    reset(pos);
+    for (uint32_t guard = 0; guard < 4096; ++guard) {
+        if (stored_now) {
+            // LEN NLEN at `pos` (byte aligned), then the bytes
+            if (pos + 32 > end_bits) break;
+            fill();
+            const uint32_t v = take(32);
+            const uint32_t L = v & 0xffffu;
+            if (L != ((v >> 16) ^ 0xffffu)) break;
+            const uint32_t nxt = pos + 8 * L;
+            if (nxt >= end_bits) break;
+            reset(nxt);
+            stored_now = false;
+        }
+        // a block header at pos
+        if (pos >= next_bit || pos + 3 > end_bits) break;
+        fill();
+        const uint32_t h = take(3);
+        if (h & 1) break;   // a final block: nothing after it
+        const uint32_t type = h >> 1;
+        if (type == 0) {
+            const uint32_t lb = (pos + 7) & ~7u;   // the LEN field
+            if (lb >= next_bit) break;             // the next candidate's block: its walk
+            record(lb, KIND_STORED);
+            reset(lb);
+            stored_now = true;
+            continue;
+        }
+        if (type != 1) {   // dynamic (or invalid): a candidate, and the walk ends
+            if (type == 2) record(pos - 3, KIND_DYN);
+            break;
+        }
+        record(pos - 3, KIND_FIXED);
+        // the fixed block's symbols up to its end-of-block
+        bool ok = false;
+        for (uint32_t n = 0; n < 65536; ++n) {
+            fill();
+            if (pos + 7 > end_bits) break;
+            const uint32_t c9 = __builtin_bitreverse32((uint32_t)bb) >> 23;   // the next 9 code bits, first bit high
+            uint32_t L, sym;
+            if ((c9 >> 2) < 24) {
+                L = 7;
+                sym = 256 + (c9 >> 2);
+            } else if ((c9 >> 1) < 192) {
+                L = 8;
+                sym = (c9 >> 1) - 48;
+            } else if ((c9 >> 1) < 200) {
+                L = 8;
+                sym = 280 + (c9 >> 1) - 192;
+            } else {
+                L = 9;
+                sym = 144 + c9 - 400;
+            }
+            take(L);
+            if (sym == 256) {
+                ok = true;
+                break;
+            }
+            if (sym < 256) continue;
+            if (sym > 285) break;   // invalid literal/length code
+            const uint32_t li = sym - 257;
+            const uint32_t xl = (li < 8 || li == 28) ? 0u : ((li - 4) >> 2);
+            fill();
+            take(xl);
+            const uint32_t dsym = __builtin_bitreverse32((uint32_t)bb) >> 27;
+            take(5);
+            if (dsym >= 30) break;   // invalid distance code
+            const uint32_t xd = dsym < 4 ? 0u : (dsym >> 1) - 1;
+            fill();
+            take(xd);
+        }
+        if (!ok || pos > end_bits) break;
+    }
+    // the regions the walk crossed up to where it stopped hold no other start
+    settle(region_of((pos < end_bits ? pos : end_bits - 1) >> 3, st.R, st.regions));
     }
 }
 
@@ -1441,6 +1653,15 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
     const uint32_t scan_wgs = 3u * cus;
     hipLaunchKernelGGL(bp_scan_kernel<false>, dim3(scan_wgs), dim3(64 * SCAN_WAVES), 0, s, in, in_off, in_len, order,
                        rmap, fit + 1, st, tbase, tasks, marked);
+    // the skim (payloads without sync markers), then pass 2 on the regions no
+    // walk reached (BPMD_BP_SKIM=0: off, A/B only)
+    static const bool skim = [] {
+        const char* e = getenv("BPMD_BP_SKIM");
+        return !(e && e[0] == '0');
+    }();
+    if (skim)
+        hipLaunchKernelGGL(bp_skim_kernel, dim3(4u * cus), dim3(256), 0, s, in, in_off, in_len, order, rmap, fit + 1, st,
+                           tbase, tasks, marked);
     hipLaunchKernelGGL(bp_scan_kernel<true>, dim3(scan_wgs), dim3(64 * SCAN_WAVES), 0, s, in, in_off, in_len, order,
                        rmap, fit + 1, st, tbase, tasks, marked);
     hipLaunchKernelGGL(bp_slots_kernel, dim3(4u * cus), dim3(256), 0, s, in_len, order, fit, st, tbase,
@@ -1451,12 +1672,15 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
     int e = bpmd_internal_inflate_lane3_seg(in, in_off, in_len, (uint32_t)cap_tasks, tasks, sym, res, raw, q + 3, wgs,
                                             s, fit + 1);
     if (e) return e;
-    // resolve: segment-parallel (chain walk, then one workgroup per payload
-    // resolving every segment at once), or the serial walk of round 4
-    // (BPMD_BP_RESOLVE=serial, A/B only)
+    // resolve: the serial walk per payload (default), or the segment-parallel
+    // form (BPMD_BP_RESOLVE=parallel; measured slower: a reference in
+    // deflated JSON usually points at a byte that was itself copied from the
+    // segment before, and so on back to the payload's first segment, so the
+    // chase through symbols runs one hop per earlier segment -- C4 8-way
+    // shard 8.6 -> 14.7 ms, profiles/r05e_resolve_ab.log)
     static const bool serial_resolve = [] {
         const char* e = getenv("BPMD_BP_RESOLVE");
-        return e && !strcmp(e, "serial");
+        return !(e && !strcmp(e, "parallel"));
     }();
     if (serial_resolve) {
         hipLaunchKernelGGL(bp_resolve_kernel, dim3(8u * cus), dim3(256), 0, s, order, fit, tbase, tasks, res,

@@ -1081,7 +1081,7 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
             // candidates this segment has passed (not headers) are dropped
             const uint32_t cur = vbase + (uint32_t)((int32_t)vtot - (tb + (int32_t)nb));
             while (nk_bit < cur) next_cand(nk, nk_left);
-            if (nk_bit == cur && nk_kind == bp::KIND_DYN) {
+            if (nk_bit == cur && (nk_kind == bp::KIND_DYN || nk_kind == bp::KIND_FIXED)) {
                 result = bp::SEG_HANDOFF;
                 st = S_DONE;
             }
