@@ -1541,10 +1541,12 @@ namespace {
 // tune: null, or deflate_stream::tune's (good_length, max_lazy, nice_length,
 // max_chain) (deflate_stream.ipp:307-317) replacing the level's table row;
 // the level still picks the parser, and the chain keeps the engine's caps
+// host_chunks >= 0: the caller knows the batch's chunk count (the per-stream
+// deflater, one message of known length), so nothing is read back
 int deflate_impl(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n, uint8_t* out,
                  const uint64_t* out_off, const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
                  uint32_t* out_bits, const uint32_t* mask_key, const uint32_t* hist_len, int level, int window_bits,
-                 int strategy, hipStream_t stream, const int* tune = nullptr)
+                 int strategy, hipStream_t stream, const int* tune = nullptr, int64_t host_chunks = -1)
 {
     bpmd::dfl::Params P;
     P.L = lz::level_params(level);
@@ -1576,6 +1578,14 @@ int deflate_impl(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_l
     if (he != hipSuccess) return (int)he;
     hipLaunchKernelGGL(count_chunks_kernel, dim3(n < 256 * 256 ? (n + 255) / 256 : 256), dim3(256), 0, stream, in_len, n,
                        all, d_total);
+    uint32_t total = 0;
+    P.chain = chain(true);
+    if (host_chunks >= 0) {
+        if (host_chunks > 0xFFFFFFFFll) return (int)hipErrorInvalidValue;
+        total = (uint32_t)host_chunks;   // the device count above is the same number
+        const int e = all ? 0 : launch_single(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, P, stream);
+        if (e) return e;
+    } else {
     // a pinned word per host thread, so the copy is asynchronous and the event covers it
     thread_local uint32_t* h_total = nullptr;
     if (!h_total && hipHostMalloc((void**)&h_total, 64, hipHostMallocDefault) != hipSuccess) return (int)hipErrorOutOfMemory;
@@ -1586,13 +1596,13 @@ int deflate_impl(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_l
         (void)hipEventDestroy(ev);
         return (int)he;
     }
-    P.chain = chain(true);
     int e = all ? 0 : launch_single(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, P, stream);
     he = hipEventSynchronize(ev);
     (void)hipEventDestroy(ev);
     if (e) return e;
     if (he != hipSuccess) return (int)he;
-    const uint32_t total = *h_total;
+    total = *h_total;
+    }
     const bool big = total > 0 || all;
     if (!big) {
         // the stitch also finishes zero-chunk messages only on the takeover path
@@ -1652,10 +1662,11 @@ extern "C" int bpmd_internal_deflate_bits_hist(const uint8_t* in, const uint64_t
                                                uint32_t n, uint8_t* out, const uint64_t* out_off,
                                                const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
                                                uint32_t* out_bits, const uint32_t* hist_len, int level,
-                                               int window_bits, int strategy, const int* tune, hipStream_t stream)
+                                               int window_bits, int strategy, const int* tune, hipStream_t stream,
+                                               int64_t host_chunks)
 {
     return deflate_impl(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, out_bits, nullptr, hist_len,
-                        level, window_bits, strategy, stream, tune);
+                        level, window_bits, strategy, stream, tune, host_chunks);
 }
 
 extern "C" int bpmd_internal_deflate_keyed(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,

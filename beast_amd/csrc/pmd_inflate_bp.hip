@@ -774,10 +774,11 @@ bp_skim_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
         last_k = k;
     };
     // bit reader: bb holds nb bits; refills take dwords from the 16-byte
-    // block q, and q is replaced by nx, which was loaded one block ahead, so
-    // a refill does not wait on memory once the walk is under way
-    uint4 q = make_uint4(0, 0, 0, 0), nx = q;
-    uint32_t qi = 0, bi = 0;   // dword index in q; block index of nx
+    // block q; the next three blocks are already loading (a fixed block of
+    // near-random bytes uses a block every ~14 symbols, and one block ahead
+    // left the walk waiting on memory at every block)
+    uint4 q = make_uint4(0, 0, 0, 0), n1 = q, n2 = q, n3 = q;
+    uint32_t qi = 0, bi = 0;   // dword index in q; block index of n3
     uint64_t bb = 0;
     uint32_t nb = 0;
     auto load_block = [&](uint32_t b) -> uint4 {   // 16-byte block b of A, zeros past the payload
@@ -787,8 +788,10 @@ bp_skim_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
         const uint32_t qb = B.sbits + at;
         const uint32_t blk = qb >> 7;
         q = load_block(blk);
-        nx = load_block(blk + 1);
-        bi = blk + 1;
+        n1 = load_block(blk + 1);
+        n2 = load_block(blk + 2);
+        n3 = load_block(blk + 3);
+        bi = blk + 3;
         qi = (qb >> 5) & 3u;
         const uint32_t d = qi == 0 ? q.x : qi == 1 ? q.y : qi == 2 ? q.z : q.w;
         bb = (uint64_t)(d >> (qb & 31u));
@@ -799,8 +802,10 @@ bp_skim_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
     auto fill = [&]() {
         if (nb <= 32) {
             if (qi == 4) {
-                q = nx;
-                nx = load_block(++bi);
+                q = n1;
+                n1 = n2;
+                n2 = n3;
+                n3 = load_block(++bi);
                 qi = 0;
             }
             const uint32_t d = qi == 0 ? q.x : qi == 1 ? q.y : qi == 2 ? q.z : q.w;
@@ -1398,6 +1403,7 @@ struct BpCaps {
 std::mutex g_bp_mu;
 std::vector<BpCaps> g_bp_caps;
 std::atomic<int> g_bp_fail{0};   // diagnostics: decode-workspace allocations to fail
+std::atomic<int> g_bp_skim{-1};  // the skim: -1 from BPMD_BP_SKIM, 0 off, 1 on
 
 uint8_t* dw_alloc(hipStream_t s, size_t bytes)
 {
@@ -1654,11 +1660,14 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
     hipLaunchKernelGGL(bp_scan_kernel<false>, dim3(scan_wgs), dim3(64 * SCAN_WAVES), 0, s, in, in_off, in_len, order,
                        rmap, fit + 1, st, tbase, tasks, marked);
     // the skim (payloads without sync markers), then pass 2 on the regions no
-    // walk reached (BPMD_BP_SKIM=0: off, A/B only)
-    static const bool skim = [] {
+    // walk reached (BPMD_BP_SKIM=1; off by default: see the A/B in DESIGN 4.1d)
+    int skim_mode = g_bp_skim.load();
+    if (skim_mode < 0) {
         const char* e = getenv("BPMD_BP_SKIM");
-        return !(e && e[0] == '0');
-    }();
+        skim_mode = e && e[0] == '1' ? 1 : 0;
+        g_bp_skim.store(skim_mode);
+    }
+    const bool skim = skim_mode == 1;
     if (skim)
         hipLaunchKernelGGL(bp_skim_kernel, dim3(4u * cus), dim3(256), 0, s, in, in_off, in_len, order, rmap, fit + 1, st,
                            tbase, tasks, marked);
@@ -1698,6 +1707,9 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
     return bpmd_internal_inflate_wave_ordered(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, raw,
                                               nullptr, fb, q + 2, s);
 }
+
+// the fixed-block skim on (1) or off (0) for the following calls (tests, A/B)
+extern "C" void bpmd_diag_set_bp_skim(int on) { g_bp_skim.store(on ? 1 : 0); }
 
 // diagnostics (tests): the next k decode-workspace allocations fail
 extern "C" void bpmd_diag_bp_fail_alloc(int k) { g_bp_fail.store(k); }

@@ -38,7 +38,8 @@ extern "C" int bpmd_internal_deflate_bits_hist(const uint8_t* in, const uint64_t
                                                uint32_t n, uint8_t* out, const uint64_t* out_off,
                                                const uint32_t* out_cap, uint32_t* out_len, int32_t* status,
                                                uint32_t* out_bits, const uint32_t* hist_len, int level,
-                                               int window_bits, int strategy, const int* tune, hipStream_t stream);
+                                               int window_bits, int strategy, const int* tune, hipStream_t stream,
+                                               int64_t host_chunks);
 
 struct bpmd_stream {
     bool is_deflate = true;
@@ -72,14 +73,29 @@ struct bpmd_stream {
     hipStream_t hs = nullptr;
     uint8_t* dmem = nullptr;
     size_t dcap = 0;
+    // pinned host staging for the call's copies (a copy from pageable memory
+    // is staged by the runtime and waits; from pinned memory it is one DMA)
+    uint8_t* hpin = nullptr;
+    size_t hpin_cap = 0;
 };
 
 namespace {
 
-// device block layout: [meta 64 B][input][output]
-struct DevLayout {
-    size_t in_off, out_off, total;
-};
+// the stream's pinned staging buffer, at least `need` bytes
+uint8_t* pinned(bpmd_stream* s, size_t need)
+{
+    if (need <= s->hpin_cap) return s->hpin;
+    if (s->hpin) (void)hipHostFree(s->hpin);
+    s->hpin = nullptr;
+    s->hpin_cap = 0;
+    const size_t c = std::max<size_t>(need + need / 2, 1 << 16);
+    if (hipHostMalloc((void**)&s->hpin, c, hipHostMallocDefault) != hipSuccess) {
+        s->hpin = nullptr;
+        return nullptr;
+    }
+    s->hpin_cap = c;
+    return s->hpin;
+}
 
 int ensure_device(bpmd_stream* s, size_t need)
 {
@@ -104,7 +120,11 @@ struct Meta {
 static_assert(sizeof(Meta) == 64, "meta block");
 
 // one flush's bytes through the deflate kernels with the stream's history in
-// front of them; returns 0 or a negative bpmd_result
+// front of them; returns 0 or a negative bpmd_result.  Device block:
+// [meta 64 B][output][history + input]; the host stages meta and input in
+// pinned memory, so the call is two H2D copies, the kernels (the chunk count
+// is known here, so the deflater reads nothing back), one D2H of meta and
+// output together and one wait.
 int run_one(bpmd_stream* s, const uint8_t* in, size_t n, size_t out_cap, std::vector<uint8_t>& out, int32_t& status,
             uint32_t& bits)
 {
@@ -112,30 +132,37 @@ int run_one(bpmd_stream* s, const uint8_t* in, size_t n, size_t out_cap, std::ve
     if (n + hn > 0xFFFFFFFFu || out_cap > 0xFFFFFFFFu) return BPMD_R_INVALID_ARGUMENT;
     int r = bpmd_init();
     if (r) return r;
-    const size_t in_at = 64, out_at = (in_at + hn + n + 15) & ~size_t(15);
-    if ((r = ensure_device(s, out_at + out_cap + 16)) != 0) return r;
+    const size_t out_at = 64, in_at = (out_at + out_cap + 15) & ~size_t(15), total = in_at + hn + n;
+    if ((r = ensure_device(s, total + 16)) != 0) return r;
+    uint8_t* h = pinned(s, total + 16);
+    if (!h) return BPMD_R_HIP_ERROR;
     Meta m{};
     m.in_off = hn;
     m.out_off = 0;
     m.in_len = (uint32_t)n;
     m.out_cap = (uint32_t)out_cap;
     m.hist_len = (uint32_t)hn;
+    std::memcpy(h, &m, sizeof m);
+    if (hn) std::memcpy(h + in_at, s->hist.data(), hn);
+    if (n) std::memcpy(h + in_at + hn, in, n);
     uint8_t* d = s->dmem;
-    if (hipMemcpyAsync(d, &m, sizeof m, hipMemcpyHostToDevice, s->hs) != hipSuccess) return BPMD_R_HIP_ERROR;
-    if (hn && hipMemcpyAsync(d + in_at, s->hist.data(), hn, hipMemcpyHostToDevice, s->hs) != hipSuccess)
+    if (hipMemcpyAsync(d, h, sizeof m, hipMemcpyHostToDevice, s->hs) != hipSuccess) return BPMD_R_HIP_ERROR;
+    if (hn + n && hipMemcpyAsync(d + in_at, h + in_at, hn + n, hipMemcpyHostToDevice, s->hs) != hipSuccess)
         return BPMD_R_HIP_ERROR;
-    if (n && hipMemcpyAsync(d + in_at + hn, in, n, hipMemcpyHostToDevice, s->hs) != hipSuccess) return BPMD_R_HIP_ERROR;
     Meta* dm = (Meta*)d;
+    // chunks of the chunk-parallel path: every chunk with a history window,
+    // else only messages over one chunk (pmd_deflate.hip chunk_count)
+    const int64_t chunks = hn ? (int64_t)((n + 4095) / 4096) : (n > 4096 ? (int64_t)((n + 4095) / 4096) : 0);
     const int e = bpmd_internal_deflate_bits_hist(d + in_at, &dm->in_off, &dm->in_len, 1, d + out_at, &dm->out_off,
                                                   &dm->out_cap, &dm->out_len, &dm->status, &dm->bits,
                                                   hn ? &dm->hist_len : nullptr, s->level, s->wbits, s->strategy,
-                                                  s->tuned ? s->tune4 : nullptr, s->hs);
+                                                  s->tuned ? s->tune4 : nullptr, s->hs, chunks);
     if (e) return BPMD_R_HIP_ERROR;
-    if (hipMemcpyAsync(&m, d, sizeof m, hipMemcpyDeviceToHost, s->hs) != hipSuccess) return BPMD_R_HIP_ERROR;
+    if (hipMemcpyAsync(h, d, out_at + out_cap, hipMemcpyDeviceToHost, s->hs) != hipSuccess) return BPMD_R_HIP_ERROR;
     if (hipStreamSynchronize(s->hs) != hipSuccess) return BPMD_R_HIP_ERROR;
-    out.resize(m.out_len);
-    if (m.out_len && hipMemcpy(out.data(), d + out_at, m.out_len, hipMemcpyDeviceToHost) != hipSuccess)
-        return BPMD_R_HIP_ERROR;
+    std::memcpy(&m, h, sizeof m);
+    if (m.out_len > out_cap) return BPMD_R_HIP_ERROR;
+    out.assign(h + out_at, h + out_at + m.out_len);
     status = m.status;
     bits = m.bits;
     return BPMD_R_OK;
@@ -425,11 +452,11 @@ int ensure_zstate(bpmd_stream* s, size_t n_in, size_t cap)
         if (hipMalloc(&s->din, c) != hipSuccess) return BPMD_R_HIP_ERROR;
         s->din_cap = c;
     }
-    if (cap + 64 > s->dout_cap) {
+    if (cap + 128 > s->dout_cap) {   // [result 64 B][output]
         if (s->dout) (void)hipFree(s->dout);
         s->dout = nullptr;
         s->dout_cap = 0;
-        const size_t c = std::max<size_t>(cap + cap / 2 + 64, 4096);
+        const size_t c = std::max<size_t>(cap + cap / 2 + 128, 4096);
         if (hipMalloc(&s->dout, c) != hipSuccess) return BPMD_R_HIP_ERROR;
         s->dout_cap = c;
     }
@@ -471,14 +498,27 @@ extern "C" int bpmd_inflate_stream_write(bpmd_stream* s, bpmd_zparams* zs, int f
     if ((r = ensure_zstate(s, n, cap)) != 0) return r;
     const hipStream_t hs = s->hs;
     Result res{};
-    void* dres = (uint8_t*)s->zst + sizeof(State);
-    bool ok = (n == 0 || hipMemcpyAsync(s->din, zs->next_in, n, hipMemcpyHostToDevice, hs) == hipSuccess) &&
-              bpmd_internal_zstream_write(s->zst, s->din, n, s->dout, cap, flush, dres, hs) == 0 &&
-              hipMemcpyAsync(&res, dres, sizeof res, hipMemcpyDeviceToHost, hs) == hipSuccess &&
+    // the result record and the output share one device block, so one D2H
+    // brings both back when the output is at most `spec` bytes (pinned
+    // staging for both directions: each copy is one DMA)
+    constexpr size_t RES_AT = 64;
+    const size_t spec = std::min<size_t>(cap, 16384);
+    uint8_t* h = pinned(s, std::max(n, RES_AT + spec) + 64);
+    if (!h) return BPMD_R_HIP_ERROR;
+    if (n) std::memcpy(h, zs->next_in, n);
+    bool ok = (n == 0 || hipMemcpyAsync(s->din, h, n, hipMemcpyHostToDevice, hs) == hipSuccess) &&
+              bpmd_internal_zstream_write(s->zst, s->din, n, s->dout + RES_AT, cap, flush, s->dout, hs) == 0 &&
+              hipMemcpyAsync(h, s->dout, RES_AT + spec, hipMemcpyDeviceToHost, hs) == hipSuccess &&
               hipStreamSynchronize(hs) == hipSuccess;
+    if (ok) std::memcpy(&res, h, sizeof res);
     // the bytes are in the caller's buffer whether or not done() publishes them
-    ok = ok && (res.out_used == 0 ||
-                hipMemcpy(zs->next_out, s->dout, res.out_used, hipMemcpyDeviceToHost) == hipSuccess);
+    ok = ok && res.out_used <= cap;
+    if (ok && res.out_used) {
+        std::memcpy(zs->next_out, h + RES_AT, std::min<size_t>(res.out_used, spec));
+        if (res.out_used > spec)
+            ok = hipMemcpy((uint8_t*)zs->next_out + spec, s->dout + RES_AT + spec, res.out_used - spec,
+                           hipMemcpyDeviceToHost) == hipSuccess;
+    }
     if (!ok) return BPMD_R_HIP_ERROR;   // the device state is unchanged only if the kernel never ran
     if (res.published) {
         zs->next_in = (const uint8_t*)zs->next_in + res.in_used;
@@ -495,9 +535,9 @@ extern "C" int bpmd_inflate_stream_write(bpmd_stream* s, bpmd_zparams* zs, int f
 extern "C" int bpmd_inflate_stream_footprint(const bpmd_stream* s, size_t* host_bytes, size_t* device_bytes)
 {
     if (!s || s->is_deflate) return BPMD_R_INVALID_ARGUMENT;
-    if (host_bytes) *host_bytes = 0;   // the reservoir and window live on the device
     if (device_bytes)
         *device_bytes = (s->zst ? sizeof(State) + sizeof(Result) : 0) + s->din_cap + s->dout_cap;
+    if (host_bytes) *host_bytes = s->hpin_cap;   // pinned staging only
     return BPMD_R_OK;
 }
 
@@ -509,6 +549,7 @@ extern "C" void bpmd_stream_destroy(bpmd_stream* s)
     if (s->zst) (void)hipFree(s->zst);
     if (s->din) (void)hipFree(s->din);
     if (s->dout) (void)hipFree(s->dout);
+    if (s->hpin) (void)hipHostFree(s->hpin);
     if (s->hs) {
         bpmd_internal_scratch_release(s->hs);
         (void)hipStreamDestroy(s->hs);

@@ -433,8 +433,9 @@ int bpmd_inflate_stream_clear(bpmd_stream* s);
  * every call.  A data error returns without advancing z_params, as the
  * reference's err() does (inflate_stream.ipp:120-125). */
 int bpmd_inflate_stream_write(bpmd_stream* s, bpmd_zparams* zs, int flush);
-/* Memory an inflate stream holds (host: none; device: state + window and the
- * call's input/output buffers); no reference counterpart, for bounded-memory tests. */
+/* Memory an inflate stream holds (host: the pinned staging buffer of the
+ * call's copies, no decoder state; device: state + window and the call's
+ * input/output buffers); no reference counterpart, for bounded-memory tests. */
 int bpmd_inflate_stream_footprint(const bpmd_stream* s, size_t* host_bytes, size_t* device_bytes);
 void bpmd_stream_destroy(bpmd_stream* s);
 

@@ -334,3 +334,30 @@ def test_deep_reference_chains(mode):
             caps.append(size)
     _check(payloads, caps)
     _check(payloads, caps, raw=True)
+
+
+@pytest.mark.parametrize("level", [1, 6])
+def test_fixed_block_skim(mode, level):
+    """The fixed-block skim (off by default; bpmd_diag_set_bp_skim): Beast's
+    near-random payloads are runs of stored and fixed blocks, and the walks
+    from pass 1's stored candidates record every block start they pass.
+    Results must stay the serial decoder's, including capacity cuts and
+    corrupted payloads (a walk only ever adds candidates)."""
+    pmd = _pmd()
+    rng = random.Random(0x5C1 + level)
+    payloads, caps = [], []
+    for i in range(40):
+        size = rng.choice([20000, 65536, 100000])
+        data = _data(rng.choice(["binary", "random", "json"]), size, 500 + i)
+        payloads.append(O.pmd_deflate(data, level, 15, rng.choice([1, 4, 8])))
+        caps.append(size if i % 5 else rng.randrange(1, size))
+    for i in range(0, 40, 7):   # a few corrupted ones
+        q = bytearray(payloads[i])
+        q[rng.randrange(len(q))] ^= 1 << rng.randrange(8)
+        payloads[i] = bytes(q)
+    pmd.lib().bpmd_diag_set_bp_skim(1)
+    try:
+        _check(payloads, caps)
+        _check(payloads, caps, raw=True)
+    finally:
+        pmd.lib().bpmd_diag_set_bp_skim(0)

@@ -175,7 +175,8 @@ def test_c1_connection_bounded_memory():
     finally:
         g.close()
     (h0, d0), (h1, d1) = feet
-    assert h1 == h0 == 0 and d1 == d0 and d1 < 1 << 20, feet
+    # host: only the pinned staging of the call's copies (no decoder state)
+    assert h1 == h0 and h0 < 1 << 20 and d1 == d0 and d1 < 1 << 20, feet
 
 
 def test_many_small_writes():
