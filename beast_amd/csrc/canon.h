@@ -51,6 +51,33 @@ __device__ __forceinline__ Sym canon_decode(const uint32_t (&Q)[NB], uint32_t c)
     return r;
 }
 
+// A code uses few distinct lengths (deflated JSON: about 8-10 for
+// literal/length, 5-7 for distances), and a length with no codes adds a word
+// that can never win the search (its lim equals the length before it).  The
+// compact form keeps only the words of lengths that have codes, in order,
+// padded with 0 (0 - (c + 1) << 15 wraps above 2^31, so padding never wins
+// and an invalid code still reads as invalid): the same result as
+// canon_min<15> in K - 1 instead of 14 subtractions and mins.  Returns false
+// when the code has more than K distinct lengths (the caller keeps the full
+// search for it).
+template <int NB, int K>
+__device__ __forceinline__ bool compact_canon(const uint32_t (&Q)[NB], uint32_t (&W)[K])
+{
+    uint32_t rank = 0, prev = 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) W[j] = 0;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        const uint32_t lim = Q[i] >> 15;
+        const bool used = lim != prev;
+        prev = lim;
+#pragma unroll
+        for (int j = 0; j < K; ++j) W[j] = (used && rank == (uint32_t)j) ? Q[i] : W[j];
+        rank += used ? 1u : 0u;
+    }
+    return rank <= (uint32_t)K;
+}
+
 // The reference's slow path asks for the root bits, or for root + sub-table
 // index bits when the code is longer than the root: a sub-table covers one
 // root prefix and is as deep as the longest code under it, i.e. the length

@@ -457,7 +457,7 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
                const uint32_t* __restrict__ in_len, const uint32_t* __restrict__ order,
                const uint32_t* __restrict__ region_map, const uint32_t* __restrict__ n_regions_dev,
                const Stat* __restrict__ stats, const uint32_t* __restrict__ task_base, SegTask* __restrict__ tasks,
-               uint32_t* __restrict__ marked)
+               uint32_t* __restrict__ marked, uint32_t dyn_stride)
 {
     __shared__ ScanLds L;
     const uint32_t n_regions = *n_regions_dev;
@@ -477,11 +477,18 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
     for (uint32_t g0 = (blockIdx.x * SCAN_WAVES + wv) * step; g0 < n_regions; g0 += waves * step) {
     uint64_t todo = 1;
     if (DYN) {
-        // only the regions pass 1 left pending, of unmarked payloads
+        // only the regions pass 1 left pending, of unmarked payloads, and of
+        // those every dyn_stride-th: a dynamic-header search costs a region's
+        // whole bit-offset scan, and payloads without sync markers decode
+        // faster as fewer, longer segments than they scan as many (C4 8-way
+        // shard of Beast's payloads at 1 / 2 / 4 segments per lane: 13.5 /
+        // 16.1 / 15.7 ms, this library's payloads 10.9 / 9.5 / 8.7 ms,
+        // profiles/r05h_bp_segs_sweep.log)
         const uint32_t gl = g0 + lane;
         bool need = false;
         if (gl < n_regions && tasks[gl].kind == KIND_PENDING) {
-            if (marked[region_map[gl]]) tasks[gl].kind = KIND_NONE;
+            const uint32_t ri = region_map[gl];
+            if (marked[ri] || (gl - task_base[ri]) % dyn_stride != 0) tasks[gl].kind = KIND_NONE;
             else need = true;
         }
         todo = __ballot(need);
@@ -1657,8 +1664,14 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
     // workgroups per CU by LDS; then the slots, one wave per payload
     hipLaunchKernelGGL(bp_region_map_kernel, dim3((n + 255) / 256), dim3(256), 0, s, fit, reg, tbase, rmap);
     const uint32_t scan_wgs = 3u * cus;
+    // BPMD_BP_DYN_STRIDE: pass 2 searches every n-th pending region (default 4)
+    static const uint32_t dyn_stride = [] {
+        const char* e = getenv("BPMD_BP_DYN_STRIDE");
+        const uint32_t v = e ? (uint32_t)strtoul(e, nullptr, 10) : 0u;
+        return v ? v : 4u;
+    }();
     hipLaunchKernelGGL(bp_scan_kernel<false>, dim3(scan_wgs), dim3(64 * SCAN_WAVES), 0, s, in, in_off, in_len, order,
-                       rmap, fit + 1, st, tbase, tasks, marked);
+                       rmap, fit + 1, st, tbase, tasks, marked, dyn_stride);
     // the skim (payloads without sync markers), then pass 2 on the regions no
     // walk reached (BPMD_BP_SKIM=1; off by default: see the A/B in DESIGN 4.1d)
     int skim_mode = g_bp_skim.load();
@@ -1672,7 +1685,7 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
         hipLaunchKernelGGL(bp_skim_kernel, dim3(4u * cus), dim3(256), 0, s, in, in_off, in_len, order, rmap, fit + 1, st,
                            tbase, tasks, marked);
     hipLaunchKernelGGL(bp_scan_kernel<true>, dim3(scan_wgs), dim3(64 * SCAN_WAVES), 0, s, in, in_off, in_len, order,
-                       rmap, fit + 1, st, tbase, tasks, marked);
+                       rmap, fit + 1, st, tbase, tasks, marked, dyn_stride);
     hipLaunchKernelGGL(bp_slots_kernel, dim3(4u * cus), dim3(256), 0, s, in_len, order, fit, st, tbase,
                        wbase, tasks);
     if (hipGetLastError() != hipSuccess) return (int)hipErrorUnknown;

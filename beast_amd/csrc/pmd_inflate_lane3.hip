@@ -94,6 +94,15 @@ constexpr int KLIT = BPMD3_KLIT;   // symbols decoded per iteration when literal
 #ifndef BPMD3_KCL
 #define BPMD3_KCL 6
 #endif
+// compact canonical search (canon.h compact_canon): words per literal/length
+// and distance table (0: the full 15-word search only)
+#ifndef BPMD3_CKL
+#define BPMD3_CKL 11
+#endif
+#ifndef BPMD3_CKD
+#define BPMD3_CKD 8
+#endif
+constexpr int CKL = BPMD3_CKL > 0 ? BPMD3_CKL : 1, CKD = BPMD3_CKD > 0 ? BPMD3_CKD : 1;
 constexpr int KCL = BPMD3_KCL;   // code-length symbols per iteration (pass 1; a refill before each, <= 4 input dwords per iteration)
 #ifndef BPMD3_KNIB
 #define BPMD3_KNIB 32
@@ -783,6 +792,13 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
     bool last = false, fin = true;   // fin: END token written
     uint32_t pos = 0, head = 0;
     Canon<15> tl, td;
+    // the compact words of tl / td and whether they cover the whole code
+    uint32_t WL[CKL], WD[CKD];
+    bool wide = BPMD3_CKL == 0;
+#pragma unroll
+    for (int i = 0; i < CKL; ++i) WL[i] = 0;
+#pragma unroll
+    for (int i = 0; i < CKD; ++i) WD[i] = 0;
     Canon<7> tc;
     // header state
     uint32_t nlen = 0, ndist = 0, want = 0, have = 0, prev = 0;
@@ -862,6 +878,10 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
         pos = 0;
 #pragma unroll
         for (int i = 0; i < 15; ++i) { tl.Q[i] = 0; td.Q[i] = 0; }
+#pragma unroll
+        for (int i = 0; i < CKL; ++i) WL[i] = 0;
+#pragma unroll
+        for (int i = 0; i < CKD; ++i) WD[i] = 0;
         tl.root = 9;
         td.root = 5;
 #pragma unroll
@@ -899,10 +919,13 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
         uint32_t kp[KLIT + 1], kc[KLIT], kL[KLIT], kx[KLIT];
         bool kinv[KLIT];
         kp[0] = 0;
+        // (a wave-uniform choice: the full search only while some lane's
+        // tables have more distinct lengths than the compact words hold)
+        const bool any_wide = BPMD3_CKL == 0 || __ballot(wide) != 0;
 #pragma unroll
         for (int k = 0; k < KLIT; ++k) {
             kc[k] = rev15(w >> kp[k]);
-            const Sym y = canon_decode<15>(tl.Q, kc[k]);
+            const Sym y = any_wide ? canon_decode<15>(tl.Q, kc[k]) : canon_decode<CKL>(WL, kc[k]);
             kL[k] = y.L;
             kx[k] = y.idx;
             kinv[k] = y.inval;
@@ -968,7 +991,7 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
         len += (uint32_t)(w2 >> L) & lowmask(xl);
         const uint32_t used = L + (is_len ? xl : 0u);
         const uint32_t d15 = rev15(w2 >> used);
-        const Sym yd = canon_decode<15>(td.Q, d15);
+        const Sym yd = any_wide ? canon_decode<15>(td.Q, d15) : canon_decode<CKD>(WD, d15);
         const uint32_t Ld = yd.L;
         const uint32_t dsym = *lb(T, O_DST + yd.idx);
         const bool invd = yd.inval || dsym >= 30;
@@ -1131,6 +1154,12 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
                             tl.Q[i] = kFixL[i];
                             td.Q[i] = kFixD[i];
                         }
+                        // fixed: literal/length lengths 7, 8, 9; distances 5
+#pragma unroll
+                        for (int i = 0; i < CKL; ++i) WL[i] = i < 3 ? kFixL[6 + i] : 0u;
+#pragma unroll
+                        for (int i = 0; i < CKD; ++i) WD[i] = i < 1 ? kFixD[4] : 0u;
+                        wide = BPMD3_CKL == 0;
                         tl.root = 9;
                         td.root = 5;
                         st = S_DATA;
@@ -1395,6 +1424,11 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
 #pragma unroll
                     for (int l = 1; l < 16; ++l) c[l] = (h[l] >> 20) & 0x3ffu;
                     e = make_canon<15>(c, 6, 2, td);
+                }
+                if (!e && BPMD3_CKL) {
+                    const bool okl = compact_canon<15, CKL>(tl.Q, WL);
+                    const bool okd = compact_canon<15, CKD>(td.Q, WD);
+                    wide = !(okl && okd);
                 }
                 if (e) {
                     result = e;
