@@ -38,7 +38,10 @@ struct Sym {
     bool inval;
 };
 
-template <int NB>
+// NB words; BITS: the code width c is read at (the longest length, 15 for
+// literal/length and distance codes, 7 for the code-length code) -- equal to
+// NB except for the compact words below
+template <int NB, int BITS = NB>
 __device__ __forceinline__ Sym canon_decode(const uint32_t (&Q)[NB], uint32_t c)
 {
     const uint32_t m = canon_min<NB>(Q, c);
@@ -46,7 +49,7 @@ __device__ __forceinline__ Sym canon_decode(const uint32_t (&Q)[NB], uint32_t c)
     r.inval = (m >> 31) != 0;
     const uint32_t q = m + ((c + 1) << 15);
     r.L = (q >> 11) & 15u;
-    const int32_t below = (int32_t)(c - (q >> 15)) >> (NB - (int32_t)r.L);   // in [-count_L, -1]
+    const int32_t below = (int32_t)(c - (q >> 15)) >> (BITS - (int32_t)r.L);   // in [-count_L, -1]
     r.idx = r.inval ? 0u : (uint32_t)((int32_t)(q & 0x7ffu) + below);
     return r;
 }

@@ -925,7 +925,7 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
 #pragma unroll
         for (int k = 0; k < KLIT; ++k) {
             kc[k] = rev15(w >> kp[k]);
-            const Sym y = any_wide ? canon_decode<15>(tl.Q, kc[k]) : canon_decode<CKL>(WL, kc[k]);
+            const Sym y = any_wide ? canon_decode<15>(tl.Q, kc[k]) : canon_decode<CKL, 15>(WL, kc[k]);
             kL[k] = y.L;
             kx[k] = y.idx;
             kinv[k] = y.inval;
@@ -991,7 +991,7 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
         len += (uint32_t)(w2 >> L) & lowmask(xl);
         const uint32_t used = L + (is_len ? xl : 0u);
         const uint32_t d15 = rev15(w2 >> used);
-        const Sym yd = any_wide ? canon_decode<15>(td.Q, d15) : canon_decode<CKD>(WD, d15);
+        const Sym yd = any_wide ? canon_decode<15>(td.Q, d15) : canon_decode<CKD, 15>(WD, d15);
         const uint32_t Ld = yd.L;
         const uint32_t dsym = *lb(T, O_DST + yd.idx);
         const bool invd = yd.inval || dsym >= 30;
