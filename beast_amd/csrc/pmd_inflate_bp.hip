@@ -478,11 +478,8 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
     uint64_t todo = 1;
     if (DYN) {
         // only the regions pass 1 left pending, of unmarked payloads, and of
-        // those every dyn_stride-th: a dynamic-header search costs a region's
-        // whole bit-offset scan, and payloads without sync markers decode
-        // faster as fewer, longer segments than they scan as many (C4 8-way
-        // shard of Beast's payloads at 1 / 2 / 4 segments per lane: 13.5 /
-        // 16.1 / 15.7 ms, this library's payloads 10.9 / 9.5 / 8.7 ms,
+        // those every dyn_stride-th (a dynamic-header search costs a region's
+        // whole bit-offset scan; BPMD_BP_SEGS sweep of Beast's payloads,
         // profiles/r05h_bp_segs_sweep.log)
         const uint32_t gl = g0 + lane;
         bool need = false;
@@ -1664,11 +1661,13 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
     // workgroups per CU by LDS; then the slots, one wave per payload
     hipLaunchKernelGGL(bp_region_map_kernel, dim3((n + 255) / 256), dim3(256), 0, s, fit, reg, tbase, rmap);
     const uint32_t scan_wgs = 3u * cus;
-    // BPMD_BP_DYN_STRIDE: pass 2 searches every n-th pending region (default 4)
+    // BPMD_BP_DYN_STRIDE: pass 2 searches every n-th pending region (default
+    // 1; 4 measured C4 8-way Beast shard 16.6 -> 17.8 ms, C5 17.6 -> 15.7 ms,
+    // profiles/r05j_ab_compact_canon.log)
     static const uint32_t dyn_stride = [] {
         const char* e = getenv("BPMD_BP_DYN_STRIDE");
         const uint32_t v = e ? (uint32_t)strtoul(e, nullptr, 10) : 0u;
-        return v ? v : 4u;
+        return v ? v : 1u;
     }();
     hipLaunchKernelGGL(bp_scan_kernel<false>, dim3(scan_wgs), dim3(64 * SCAN_WAVES), 0, s, in, in_off, in_len, order,
                        rmap, fit + 1, st, tbase, tasks, marked, dyn_stride);

@@ -95,9 +95,14 @@ constexpr int KLIT = BPMD3_KLIT;   // symbols decoded per iteration when literal
 #define BPMD3_KCL 6
 #endif
 // compact canonical search (canon.h compact_canon): words per literal/length
-// and distance table (0: the full 15-word search only)
+// and distance table (0, the default: the full 15-word search only).
+// Measured slower on C2 (11 / 8 words: 163-167, 9 / 7: 172, off: 190-191
+// GiB/s, three interleaved runs, profiles/r05j_ab_compact_canon.log): the
+// compact words are 27 more VGPRs live across the loop (208 vs 181) and a
+// wave-uniform branch per decode, which cost more than the 9 subtractions
+// and mins they save.
 #ifndef BPMD3_CKL
-#define BPMD3_CKL 11
+#define BPMD3_CKL 0
 #endif
 #ifndef BPMD3_CKD
 #define BPMD3_CKD 8
