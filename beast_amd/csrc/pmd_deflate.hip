@@ -1503,9 +1503,15 @@ deflate_chunks1_kernel(const uint8_t* __restrict__ in, const uint64_t* __restric
             uint32_t bit = 0, cv = 0;
             bool ovf = o.overflow;
             if (c > 0) {
-                unsigned long long v;
-                while (!((v = __hip_atomic_load(&ends[k - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & PUB))
+                // (bounded: a wait that outlived any real chunk -- seconds --
+                // ends the message as need_buffers rather than hanging)
+                unsigned long long v = 0;
+                for (uint32_t spin = 0; spin < (1u << 26); ++spin) {
+                    v = __hip_atomic_load(&ends[k - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (v & PUB) break;
                     __builtin_amdgcn_s_sleep(2);
+                }
+                if (!(v & PUB)) v = PUB | OVF;
                 ovf = ovf || (v & OVF);
                 bit = (uint32_t)(v >> 8);
                 cv = (uint32_t)v & 0xffu;
