@@ -86,11 +86,32 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
             if (ib0 + k < n_in) *(uint4*)(L.ist + k) = *(const uint4*)(in + ib0 + k);
         wave_sync();
     };
-    // bit reservoir, bitstream.hpp: v_ holds n_ bits, bytes enter at bit n_
+    // bit reservoir, bitstream.hpp: v_ holds n_ bits, bytes enter at bit n_.
+    // The bytes come from the staging buffer through a register prefetch of
+    // up to 8 bytes (one LDS round trip per 5-8 bytes instead of one per
+    // byte); only the reference's own ip / bn / bv are state, so the bytes
+    // each call consumes are unchanged (the prefetch is refilled whenever ip
+    // moves other than byte by byte: rewind, stored-block copies)
     uint32_t bv = h.bv, bn = h.bn;
+    uint64_t pfv = 0, pfip = ~0ull;   // bytes [pfip, pfip + pfn) of the input in pfv
+    uint32_t pfn = 0;
     auto pull = [&]() {
-        if (ip < ib0 || ip >= ib1) stage(ip);
-        const uint32_t b = uni(L.ist[ip - ib0]);
+        if (ip != pfip || pfn == 0) {
+            if (ip < ib0 || ip >= ib1) stage(ip);
+            const uint32_t off = (uint32_t)(ip - ib0);
+            const uint32_t a = off & ~3u;
+            const uint32_t d0 = uni(*(const uint32_t*)(L.ist + a));
+            const uint32_t d1 = a + 8 <= IST ? uni(*(const uint32_t*)(L.ist + a + 4)) : 0u;
+            pfv = (((uint64_t)d1 << 32) | d0) >> (8 * (off & 3u));
+            const uint64_t staged = ib1 - ip;
+            const uint32_t have = (a + 8 <= IST ? 8u : 4u) - (off & 3u);
+            pfn = (uint32_t)(staged < have ? staged : have);
+            pfip = ip;
+        }
+        const uint32_t b = (uint32_t)pfv & 0xffu;
+        pfv >>= 8;
+        --pfn;
+        ++pfip;
         ++ip;
         if (bn < 32) bv += b << bn;
         bn += 8;
