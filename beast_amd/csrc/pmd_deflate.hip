@@ -1802,9 +1802,13 @@ int deflate_impl(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_l
     }
     // workspace: first[n + 1] | items[total] | bits[total] | slots[total] | scan temp
     // (single write: ends[total] in place of bits and slots)
+    // the single-write chunk kernel (BPMD_DEFLATE_STITCH=0) measured slower
+    // than the stitch: a chunk's wave waits, holding its CU slot, for the
+    // chunk before it to finish encoding (C4 26.6 -> 23.8, C5 L1 27.6 -> 25.5
+    // GiB/s, profiles/r05k_ab_single_write.log); the stitch stays the default
     static const bool stitch = [] {
         const char* e = getenv("BPMD_DEFLATE_STITCH");
-        return e && e[0] == '1';
+        return !(e && e[0] == '0');
     }();
     size_t cub_bytes = 0;
     hipcub::CountingInputIterator<uint32_t> idx(0);

@@ -10,7 +10,7 @@ timeout -k 10 700 python -u -m pytest tests/test_gpu_deflate.py tests/test_gpu_c
 tail -2 $OUT/pytest.log
 for r in 1 2; do
   for v in stitch single; do
-    if [ $v = stitch ]; then export BPMD_DEFLATE_STITCH=1; else unset BPMD_DEFLATE_STITCH; fi
+    if [ $v = stitch ]; then export BPMD_DEFLATE_STITCH=1; else export BPMD_DEFLATE_STITCH=0; fi
     bash scripts/run_bench.sh ${TAG}_ab_${v}_$r 600 "d['deflate']['deflate_value'], [(k, v.get('deflate_value'), v.get('ratio_rank_local')) for k, v in d['mixed'].items() if isinstance(v, dict)]" \
       --steps 5 --warmup 1 --no-cpu-baseline --no-frame --no-exact --no-virtual-shards --no-beast-payloads || exit 2
   done
