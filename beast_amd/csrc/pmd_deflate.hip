@@ -1730,6 +1730,12 @@ int launch_single(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_
 }  // namespace
 
 namespace {
+std::atomic<int> g_single_write{-1};   // -1 from BPMD_DEFLATE_STITCH, 0 stitch, 1 single write
+}  // namespace
+// tests / A/B: the single-write chunk kernel (1) or the stitch (0)
+extern "C" void bpmd_diag_set_deflate_single_write(int on) { g_single_write.store(on ? 1 : 0); }
+
+namespace {
 // tune: null, or deflate_stream::tune's (good_length, max_lazy, nice_length,
 // max_chain) (deflate_stream.ipp:307-317) replacing the level's table row;
 // the level still picks the parser, and the chain keeps the engine's caps
@@ -1806,10 +1812,13 @@ int deflate_impl(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_l
     // than the stitch: a chunk's wave waits, holding its CU slot, for the
     // chunk before it to finish encoding (C4 26.6 -> 23.8, C5 L1 27.6 -> 25.5
     // GiB/s, profiles/r05k_ab_single_write.log); the stitch stays the default
-    static const bool stitch = [] {
+    int sm = g_single_write.load();
+    if (sm < 0) {
         const char* e = getenv("BPMD_DEFLATE_STITCH");
-        return !(e && e[0] == '0');
-    }();
+        sm = e && e[0] == '0' ? 1 : 0;
+        g_single_write.store(sm);
+    }
+    const bool stitch = sm == 0;
     size_t cub_bytes = 0;
     hipcub::CountingInputIterator<uint32_t> idx(0);
     hipcub::TransformInputIterator<uint32_t, ChunkCountOp, hipcub::CountingInputIterator<uint32_t>> counts(
