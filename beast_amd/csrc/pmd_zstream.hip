@@ -153,9 +153,25 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
     };
     bool winld = false;
     auto load_window = [&]() {   // window byte k back sits at ring position -k
+        // ring position HR - wsize + t takes window byte (wpos - wsize + t) mod
+        // wcap: 16 bytes per lane per step from t0 on (t0: the first t whose
+        // ring position is 16-byte aligned), single bytes before t0 and where
+        // a 16-byte run wraps around the window's end
         wave_sync();
-        for (uint32_t k = 1 + lane; k <= h.wsize; k += WAVE)
-            L.hist[(HR - k) & HM] = st->win[(h.wpos - k) & (wcap - 1)];
+        const uint32_t ws = h.wsize, s0 = (h.wpos - ws) & (wcap - 1);
+        const uint32_t t0 = ws & 15u;   // (all of it when ws < 16)
+        for (uint32_t t = lane; t < t0; t += WAVE) L.hist[(HR - ws + t) & HM] = st->win[(s0 + t) & (wcap - 1)];
+        for (uint32_t t = t0 + 16 * lane; t < ws; t += 16 * WAVE) {
+            const uint32_t src = (s0 + t) & (wcap - 1);
+            const uint32_t dst = (HR - ws + t) & HM;
+            if (t + 16 <= ws && src + 16 <= wcap) {
+                typedef uint4 uint4_un __attribute__((aligned(1)));
+                *(uint4*)(L.hist + dst) = *(const uint4_un*)(st->win + src);
+            } else {
+                for (uint32_t j = 0; j < 16 && t + j < ws; ++j)
+                    L.hist[(dst + j) & HM] = st->win[(src + j) & (wcap - 1)];
+            }
+        }
         winld = true;
         wave_sync();
     };
