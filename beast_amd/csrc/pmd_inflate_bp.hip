@@ -983,6 +983,13 @@ typedef uint4 uint4_ua __attribute__((aligned(1)));
 
 
 typedef uint2 uint2_sa __attribute__((aligned(2)));
+// symbols per lane per step of the serial resolve (16: round 4; a step is
+// one dependent round trip -- symbols, then the bytes references read --
+// so the longest payloads' step count sets the kernel's end)
+#ifndef BPMD_BP_RSYM
+#define BPMD_BP_RSYM 32
+#endif
+constexpr uint32_t RSYM = BPMD_BP_RSYM;
 
 __global__ void __launch_bounds__(256)
 bp_resolve_kernel(const uint32_t* __restrict__ order, const uint32_t* __restrict__ nlong,
@@ -1017,25 +1024,25 @@ bp_resolve_kernel(const uint32_t* __restrict__ order, const uint32_t* __restrict
             const uint32_t n = r.nsym;
             const uint32_t room = cap - P;   // P <= cap
             uint32_t bad = n;                // first symbol referring before the payload
-            // 16 symbols per lane per step, all loads in flight together
-            for (uint32_t c = 0; c < n; c += 1024) {
-                const uint32_t j0 = c + 16 * lane;
-                uint32_t v[16];
-                if (j0 + 16 <= n) {
+            // RSYM symbols per lane per step, all loads in flight together
+            for (uint32_t c = 0; c < n; c += 64 * RSYM) {
+                const uint32_t j0 = c + RSYM * lane;
+                uint32_t v[RSYM];
+                if (j0 + RSYM <= n) {
 #pragma unroll
-                    for (int h = 0; h < 4; ++h) {
+                    for (int h = 0; h < (int)RSYM / 4; ++h) {
                         const uint2 w = *(const uint2_sa*)(sy + j0 + 4 * h);
                         v[4 * h] = w.x & 0xffffu; v[4 * h + 1] = w.x >> 16;
                         v[4 * h + 2] = w.y & 0xffffu; v[4 * h + 3] = w.y >> 16;
                     }
                 } else {
 #pragma unroll
-                    for (int q = 0; q < 16; ++q) v[q] = j0 + q < n ? sy[j0 + q] : 0u;
+                    for (int q = 0; q < (int)RSYM; ++q) v[q] = j0 + q < n ? sy[j0 + q] : 0u;
                 }
                 uint32_t lbad = 0xffffffffu;
-                uint32_t bytes[16];
+                uint32_t bytes[RSYM];
 #pragma unroll
-                for (int q = 0; q < 16; ++q) {
+                for (int q = 0; q < (int)RSYM; ++q) {
                     const uint32_t x = v[q];
                     bytes[q] = x & 0xffu;
                     if (j0 + q < n && (x & SYM_REF)) {
@@ -1054,22 +1061,24 @@ bp_resolve_kernel(const uint32_t* __restrict__ order, const uint32_t* __restrict
                     mb = y < mb ? y : mb;
                 }
                 const uint32_t upto = (mb < n ? mb : n) < room ? (mb < n ? mb : n) : room;
-                if (j0 + 16 <= upto) {
-                    uint32_t d4[4];
+                if (j0 + RSYM <= upto) {
+                    uint32_t d4[RSYM / 4];
 #pragma unroll
-                    for (int h = 0; h < 4; ++h)
+                    for (int h = 0; h < (int)RSYM / 4; ++h)
                         d4[h] = bytes[4 * h] | (bytes[4 * h + 1] << 8) | (bytes[4 * h + 2] << 16) | (bytes[4 * h + 3] << 24);
-                    *(uint4_ua*)(o + P + j0) = make_uint4(d4[0], d4[1], d4[2], d4[3]);
+                    #pragma unroll
+                    for (int h = 0; h < (int)RSYM / 16; ++h)
+                        *(uint4_ua*)(o + P + j0 + 16 * h) = make_uint4(d4[4 * h], d4[4 * h + 1], d4[4 * h + 2], d4[4 * h + 3]);
                 } else {
 #pragma unroll
-                    for (int q = 0; q < 16; ++q)
+                    for (int q = 0; q < (int)RSYM; ++q)
                         if (j0 + q < upto) o[P + j0 + q] = (uint8_t)bytes[q];
                 }
                 if (mb != 0xffffffffu) {
                     bad = mb;
                     break;
                 }
-                if (c + 1024 > room) break;   // the rest lies past the capacity
+                if (c + 64 * RSYM > room) break;   // the rest lies past the capacity
             }
             if (bad < n) {
                 // the token at P + bad has a distance past the output so far
