@@ -983,11 +983,13 @@ typedef uint4 uint4_ua __attribute__((aligned(1)));
 
 
 typedef uint2 uint2_sa __attribute__((aligned(2)));
-// symbols per lane per step of the serial resolve (16: round 4; a step is
-// one dependent round trip -- symbols, then the bytes references read --
-// so the longest payloads' step count sets the kernel's end)
+// symbols per lane per step of the serial resolve (a step is one dependent
+// round trip -- symbols, then the bytes references read).  32 measured the
+// same as 16 on 8-way C4 / C5 shards (8.63 vs 8.65 ms, 2.41 vs 2.40 ms); a
+// build with 64 did not finish its first C4 shard call within 180 s and was
+// not pursued (profiles/r05n_resolve_width.log)
 #ifndef BPMD_BP_RSYM
-#define BPMD_BP_RSYM 32
+#define BPMD_BP_RSYM 16
 #endif
 constexpr uint32_t RSYM = BPMD_BP_RSYM;
 
