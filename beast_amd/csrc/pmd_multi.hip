@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/beast_pmd.h"
@@ -38,6 +39,29 @@ typedef int (*batch_fn)(const bpmd_cfg*, const uint8_t*, const uint64_t*, const 
 
 extern "C" void* bpmd_internal_stream_mutex(hipStream_t s);
 
+// one shard: its batch call, then (out_bytes) the per-shard total on the
+// shard's own stream, after its batch (scratch block 8), under the stream's
+// launch lock like every scratch user
+int run_shard(batch_fn fn, const bpmd_cfg* cfg, const bpmd_shard& s, bool want_total, unsigned long long** sum)
+{
+    if (hipSetDevice(s.device) != hipSuccess) return BPMD_R_HIP_ERROR;
+    int r = fn(cfg, s.d_in, s.d_in_off, s.d_in_len, s.n_msgs, s.d_out, s.d_out_off, s.d_out_cap, s.d_out_len,
+               s.d_status, s.stream);
+    if (r || !want_total) return r;
+    const hipStream_t hs = (hipStream_t)s.stream;
+    std::mutex* mu = (std::mutex*)bpmd_internal_stream_mutex(hs);
+    if (!mu) return BPMD_R_HIP_ERROR;
+    std::lock_guard<std::mutex> launch(*mu);
+    *sum = (unsigned long long*)bpmd_internal_scratch(hs, 256, 8);
+    if (!*sum || hipMemsetAsync(*sum, 0, sizeof(unsigned long long), hs) != hipSuccess) return BPMD_R_HIP_ERROR;
+    if (s.n_msgs) {
+        const uint32_t blocks = s.n_msgs / 256 + 1 < 1024 ? s.n_msgs / 256 + 1 : 1024;
+        hipLaunchKernelGGL(sum_lens_kernel, dim3(blocks), dim3(256), 0, hs, s.d_out_len, s.n_msgs, *sum);
+        if (hipGetLastError() != hipSuccess) return BPMD_R_HIP_ERROR;
+    }
+    return BPMD_R_OK;
+}
+
 int run_multi(batch_fn fn, const bpmd_cfg* cfg, const bpmd_shard* shards, int n_shards, uint64_t* out_bytes)
 {
     if (!cfg || n_shards < 0 || (n_shards && !shards)) return BPMD_R_INVALID_ARGUMENT;
@@ -46,38 +70,24 @@ int run_multi(batch_fn fn, const bpmd_cfg* cfg, const bpmd_shard* shards, int n_
         return BPMD_R_NO_DEVICE;
     for (int i = 0; i < n_shards; ++i)
         if (shards[i].device < 0 || shards[i].device >= count) return BPMD_R_INVALID_ARGUMENT;
-    int r = BPMD_R_OK;
     std::vector<unsigned long long*> sums((size_t)n_shards, nullptr);
-    // launch every shard; nothing here waits on a device
-    for (int i = 0; i < n_shards && r == BPMD_R_OK; ++i) {
-        const bpmd_shard& s = shards[i];
-        if (hipSetDevice(s.device) != hipSuccess) {
-            r = BPMD_R_HIP_ERROR;
-            break;
-        }
-        r = fn(cfg, s.d_in, s.d_in_off, s.d_in_len, s.n_msgs, s.d_out, s.d_out_off, s.d_out_cap, s.d_out_len,
-               s.d_status, s.stream);
-        if (r || !out_bytes) continue;
-        const hipStream_t hs = (hipStream_t)s.stream;
-        // per-shard total on the shard's own stream, after its batch (scratch
-        // block 8), under the stream's launch lock like every scratch user
-        std::mutex* mu = (std::mutex*)bpmd_internal_stream_mutex(hs);
-        if (!mu) {
-            r = BPMD_R_HIP_ERROR;
-            break;
-        }
-        std::lock_guard<std::mutex> launch(*mu);
-        sums[i] = (unsigned long long*)bpmd_internal_scratch(hs, 256, 8);
-        if (!sums[i] || hipMemsetAsync(sums[i], 0, sizeof(unsigned long long), hs) != hipSuccess) {
-            r = BPMD_R_HIP_ERROR;
-            break;
-        }
-        if (s.n_msgs) {
-            const uint32_t blocks = s.n_msgs / 256 + 1 < 1024 ? s.n_msgs / 256 + 1 : 1024;
-            hipLaunchKernelGGL(sum_lens_kernel, dim3(blocks), dim3(256), 0, hs, s.d_out_len, s.n_msgs, sums[i]);
-            if (hipGetLastError() != hipSuccess) r = BPMD_R_HIP_ERROR;
-        }
+    std::vector<int> rs((size_t)n_shards, BPMD_R_OK);
+    // every shard launched from a host thread of its own: a call that waits
+    // on its stream (a deflate batch with messages over 4 KiB reads back its
+    // chunk count) then waits beside the other shards' launches, not before
+    // them (round 4 launched the shards one after another)
+    if (n_shards == 1) {
+        rs[0] = run_shard(fn, cfg, shards[0], out_bytes != nullptr, &sums[0]);
+    } else {
+        std::vector<std::thread> th;
+        th.reserve((size_t)n_shards);
+        for (int i = 0; i < n_shards; ++i)
+            th.emplace_back([&, i] { rs[i] = run_shard(fn, cfg, shards[i], out_bytes != nullptr, &sums[i]); });
+        for (auto& t : th) t.join();
     }
+    int r = BPMD_R_OK;
+    for (int i = 0; i < n_shards; ++i)
+        if (rs[i] != BPMD_R_OK && r == BPMD_R_OK) r = rs[i];
     // gather the totals
     for (int i = 0; i < n_shards && r == BPMD_R_OK && out_bytes; ++i) {
         unsigned long long v = 0;

@@ -188,7 +188,9 @@ typedef struct bpmd_shard {
 } bpmd_shard;
 
 /* bpmd_inflate_batch / bpmd_deflate_batch on every shard, each on its own
- * device and stream, asynchronously.  out_bytes (n_shards entries, or NULL):
+ * device and stream, asynchronously; each shard is launched from a host
+ * thread of its own, so a shard whose call waits on its stream (deflate of
+ * messages over 4 KiB) does not hold back the others.  out_bytes (n_shards entries, or NULL):
  * each shard's total output bytes (sum of its d_out_len), gathered to the
  * host -- the call then waits for every shard -- so each shard's offset in
  * one global output is the exclusive prefix sum.  The current device is
