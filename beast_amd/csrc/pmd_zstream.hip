@@ -62,10 +62,40 @@ __constant__ static const uint8_t kOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5
 
 enum : int { F_BLOCK = 1, F_FINISH = 5, F_TREES = 6 };   // zlib::Flush values that change doWrite
 
+// Diagnostic build only (-DBPMD_PROF): cycles per phase and event counts,
+// summed over calls (bpmd_diag_zstream_counters; scripts/diag_zstream.py).
+// 0 entry (state in), 1 block header, 2 table builds, 3 inflate_fast, 4 window
+// load, 5 match copies, 6 done() and state out, 7 whole call, 8 input
+// staging; counts: 9 copies, 10 fast-loop tokens, 11 output bytes, 12
+// stagings, 13 calls, 14 input bytes
+#ifndef BPMD_ZSTREAM_HOST
+__device__ unsigned long long g_zprof[16];
+#endif
+#if defined(BPMD_PROF) && !defined(BPMD_ZSTREAM_HOST)
+#define ZP_NOW() ((unsigned long long)__builtin_amdgcn_s_memtime())
+#define ZP_ADD(i, v) (zp[i] += (unsigned long long)(v))
+#define ZP_DECL unsigned long long zp[16] = {};
+#define ZP_FLUSH() \
+    do { \
+        if (lane == 0) \
+            for (int i_ = 0; i_ < 16; ++i_) atomicAdd(&g_zprof[i_], zp[i_]); \
+    } while (0)
+#else
+#define ZP_NOW() 0ull
+#define ZP_ADD(i, v) ((void)0)
+#define ZP_DECL
+#define ZP_FLUSH() ((void)0)
+#endif
+
 __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __restrict__ in, uint64_t n_in,
                             uint8_t* __restrict__ out, uint64_t cap, int flush, Result* __restrict__ res)
 {
     const unsigned lane = lane_id();
+    ZP_DECL
+    const unsigned long long zt0 = ZP_NOW();
+    unsigned long long zth = zt0, ztd = 0;
+    (void)zth;
+    (void)ztd;
     Head h = st->h;
     const uint32_t wcap = 1u << h.wbits;
 
@@ -75,16 +105,21 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
     if (h.mode == LENLENS || h.mode == CODELENS)
         for (unsigned i = lane; i < kLens; i += WAVE) L.lens[i] = st->lens[i];
     bool tab_dirty = false, lens_dirty = false;
+    ZP_ADD(0, ZP_NOW() - zt0);
 
     // ---- input: bytes [ib0, ib1) of this call's input are staged in LDS
     uint64_t ip = 0, ib0 = 0, ib1 = 0;
     auto stage = [&](uint64_t at) {
+        const unsigned long long zs = ZP_NOW();
+        (void)zs;
         wave_sync();
         ib0 = at & ~(uint64_t)15;
         ib1 = ib0 + IST < n_in ? ib0 + IST : n_in;
         for (uint32_t k = lane * 16; k < IST; k += WAVE * 16)
             if (ib0 + k < n_in) *(uint4*)(L.ist + k) = *(const uint4*)(in + ib0 + k);
         wave_sync();
+        ZP_ADD(8, ZP_NOW() - zs);
+        ZP_ADD(12, 1);
     };
     // bit reservoir, bitstream.hpp: v_ holds n_ bits, bytes enter at bit n_.
     // The bytes come from the staging buffer through a register prefetch of
@@ -157,6 +192,8 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
         // wcap: 16 bytes per lane per step from t0 on (t0: the first t whose
         // ring position is 16-byte aligned), single bytes before t0 and where
         // a 16-byte run wraps around the window's end
+        const unsigned long long zw = ZP_NOW();
+        (void)zw;
         wave_sync();
         const uint32_t ws = h.wsize, s0 = (h.wpos - ws) & (wcap - 1);
         const uint32_t t0 = ws & 15u;   // (all of it when ws < 16)
@@ -174,11 +211,14 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
         }
         winld = true;
         wave_sync();
+        ZP_ADD(4, ZP_NOW() - zw);
     };
     // n bytes copied from `dist` back (window, then this call's output): the
     // history is contiguous, so byte j is history[op - dist + j mod dist]
     auto copy_back = [&](uint32_t dist, uint32_t n) {
         if (dist > op && !winld) load_window();
+        const unsigned long long zc = ZP_NOW();
+        (void)zc;
         wave_sync();
         for (uint32_t j0 = 0; j0 < n; j0 += WAVE) {
             const uint32_t j = j0 + lane;
@@ -190,6 +230,8 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
         }
         op += n;
         wave_sync();
+        ZP_ADD(5, ZP_NOW() - zc);
+        ZP_ADD(9, 1);
     };
     auto copy_in = [&](uint32_t n) {   // a stored block's bytes
         for (uint32_t done = 0; done < n;) {
@@ -206,6 +248,8 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
     // code tables into LDS; returns 0 or the zlib::error of inflate_table
     auto build = [&](int type, const uint8_t* lens, unsigned n, unsigned at, unsigned req, uint32_t& root,
                      uint32_t& used) -> int {
+        const unsigned long long zb = ZP_NOW();
+        (void)zb;
         wave_sync();
         unsigned r = 0, u = 0, lmin = 0;
         int e;
@@ -214,6 +258,7 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
         else e = build_table_wave<BUILD_DISTS>(lens, n, L.tab + at, req, L.ts, r, u, lmin);
         wave_sync();
         tab_dirty = true;
+        ZP_ADD(2, ZP_NOW() - zb);
         root = uni(r);
         used = uni(u);
         return (int)uni((uint32_t)e);
@@ -224,7 +269,10 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
         const uint64_t in_last = n_in - 5, out_last = cap - 257;
         const uint32_t lmask = (1u << h.lroot) - 1u, dmask = (1u << h.droot) - 1u;
         int32_t err = 0;
+        const unsigned long long zf = ZP_NOW();
+        (void)zf;
         do {
+            ZP_ADD(10, 1);
             if (bn < 15) {
                 pull();
                 pull();
@@ -290,6 +338,7 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
         } while (ip < in_last && op < out_last);
         if (err) h.mode = BAD;
         rewind();
+        ZP_ADD(3, ZP_NOW() - zf);
         return err;
     };
 
@@ -371,6 +420,7 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
             continue;
         }
         case TABLE:
+            zth = ZP_NOW();
             if (!fill(14)) goto done;
             h.nlen = take(5) + 257;
             h.ndist = take(5) + 1;
@@ -474,6 +524,7 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
             h.droot = droot;
             h.dtab = lused;
             h.mode = LEN_;
+            ZP_ADD(1, ZP_NOW() - zth);
             if (flush == F_TREES) goto done;
         }
             [[fallthrough]];
@@ -594,6 +645,7 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
     }
 
 done:   // the done() lambda, inflate_stream.ipp:88-119
+    ztd = ZP_NOW();
     flush_out();
     if (op && h.mode < BAD && (h.mode < CHECK || flush != F_FINISH)) {
         // window::write (window.hpp:109-141): the last min(n, capacity) bytes
@@ -608,6 +660,7 @@ done:   // the done() lambda, inflate_stream.ipp:88-119
     if (((ip == 0 && op == 0) || flush == F_FINISH) && ec == 0) ec = ST_NEED_BUFFERS;
     published = 1;
 quiet:
+    if (!ztd) ztd = ZP_NOW();
     flush_out();
     h.bv = bv;
     h.bn = bn;
@@ -623,6 +676,12 @@ quiet:
         res->data_type = data_type;
         res->published = published;
     }
+    ZP_ADD(6, ZP_NOW() - ztd);
+    ZP_ADD(7, ZP_NOW() - zt0);
+    ZP_ADD(11, op);
+    ZP_ADD(13, 1);
+    ZP_ADD(14, ip);
+    ZP_FLUSH();
 }
 
 #ifndef BPMD_ZSTREAM_HOST
@@ -648,5 +707,17 @@ extern "C" int bpmd_internal_zstream_write(void* st, const uint8_t* in, uint64_t
     hipLaunchKernelGGL(zstream_write_kernel, dim3(1), dim3(bpmd::WAVE), 0, stream, (State*)st, in, n_in, out, cap,
                        flush, (Result*)res);
     return (int)hipGetLastError();
+}
+
+// diagnostic counters (meaningful only in the -DBPMD_PROF build)
+extern "C" int bpmd_diag_zstream_counters(unsigned long long* out, int reset)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(bpmd::zst::g_zprof), sizeof(unsigned long long) * 16) != hipSuccess)
+        return -1;
+    if (reset) {
+        unsigned long long z[16] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(bpmd::zst::g_zprof), z, sizeof z) != hipSuccess) return -1;
+    }
+    return 0;
 }
 #endif

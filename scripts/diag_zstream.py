@@ -1,0 +1,56 @@
+"""Where a per-stream inflate call's time goes: the prof build's per-phase
+cycle counters of zstream_write_kernel (pmd_zstream.hip, -DBPMD_PROF) over
+configs[0]'s call pattern (1 KiB JSON messages, context takeover, the
+facade's rd_buf slices + 4-byte tail; scripts/facade_latency.py).
+    BPMD_LIB=beast_amd/libbeast_pmd_prof.so python scripts/diag_zstream.py [messages]
+"""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from beast_amd import synth  # noqa: E402
+from tests import test_gpu_stream as S  # noqa: E402
+from scripts.diag_deflate import NAMES as DNAMES  # noqa: E402
+
+NAMES = ["entry (state in)", "block header", "table builds", "inflate_fast", "window load", "match copies",
+         "done + state out", "whole call", "input staging"]
+COUNTS = ["copies", "fast tokens", "output bytes", "stagings", "calls", "input bytes"]
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 128
+    L = S._lib()
+    L.bpmd_diag_zstream_counters.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    zo, zi = S._mk(L, True, 8), S._mk(L, False)
+    data, off, ln = synth.make_batch("json", [1024] * n, seed=0x5EED0001)
+    msgs = [bytes(data[int(off[i]):int(off[i]) + 1024]) for i in range(n)]
+    L.bpmd_diag_deflate_counters.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    c = (ctypes.c_ulonglong * 16)()
+    dc = (ctypes.c_ulonglong * 24)()
+    for i, m in enumerate(msgs):
+        if i == 8:
+            L.bpmd_diag_zstream_counters(c, 1)
+            L.bpmd_diag_deflate_counters(dc, 1)
+        p = S.ws_deflate_message(L, zo, m)
+        assert S.ws_inflate_message(L, zi, p) == m, i
+    L.bpmd_diag_zstream_counters(c, 0)
+    L.bpmd_diag_deflate_counters(dc, 0)
+    k = n - 8
+    calls = max(1, c[13])
+    print(f"{k} messages, {c[13]} calls; per message: {c[14] / k:.0f} input bytes, {c[11] / k:.0f} output bytes, "
+          f"{c[10] / k:.0f} fast-loop tokens, {c[9] / k:.0f} match copies, {c[12] / k:.1f} input stagings")
+    for i, nm in enumerate(NAMES):
+        print(f"  {nm:18s} {c[i] / k:10.0f} cycles per message ({c[i] / calls:9.0f} per call)")
+    if c[9]:
+        print(f"  cycles per match copy {c[5] / c[9]:.0f}; per fast-loop token {c[3] / max(1, c[10]):.0f}")
+    print("deflate (chunk kernel phases, per message):")
+    for i in sorted(DNAMES):
+        print(f"  {DNAMES[i]:>28}: {dc[i] / k:12.0f}")
+    L.bpmd_stream_destroy(zo)
+    L.bpmd_stream_destroy(zi)
+
+
+if __name__ == "__main__":
+    main()
