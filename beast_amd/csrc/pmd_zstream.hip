@@ -55,6 +55,33 @@ struct alignas(16) Lds {
     WaveTableScratch ts;
 };
 
+// RFC 1951 §3.2.5's length and distance bases and extra bits in closed form,
+// equal to the tables at every value a K_LEN slot (0..28) or a distance K_VAL
+// slot (0..29) carries (huff_table.h); checked below at compile time.  Scalar
+// arithmetic: the tables in constant memory cost four dependent vector-memory
+// loads per match on this one-wave kernel (~60 % of a 1 KiB message's call)
+__host__ __device__ constexpr uint32_t len_extra(uint32_t c) { return c < 8u || c == 28u ? 0u : (c >> 2) - 1u; }
+__host__ __device__ constexpr uint32_t len_base(uint32_t c)
+{
+    return c < 8u ? 3u + c : c == 28u ? 258u : ((4u + (c & 3u)) << ((c >> 2) - 1u)) + 3u;
+}
+__host__ __device__ constexpr uint32_t dist_extra(uint32_t c) { return c < 4u ? 0u : (c >> 1) - 1u; }
+__host__ __device__ constexpr uint32_t dist_base(uint32_t c) { return c < 4u ? 1u + c : ((2u + (c & 1u)) << ((c >> 1) - 1u)) + 1u; }
+constexpr bool closed_forms_match()
+{
+    constexpr uint16_t lb[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
+                                 31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+    constexpr uint8_t lx[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+    constexpr uint16_t db[30] = {1,   2,   3,   4,   5,   7,    9,    13,   17,   25,   33,   49,    65,    97,    129,
+                                 193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+    for (uint32_t c = 0; c < 29; ++c)
+        if (len_base(c) != lb[c] || len_extra(c) != lx[c]) return false;
+    for (uint32_t c = 0; c < 30; ++c)
+        if (dist_base(c) != db[c] || dist_extra(c) != (c < 4 ? 0u : c / 2 - 1)) return false;
+    return true;
+}
+static_assert(closed_forms_match(), "length / distance closed forms");
+
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 __device__ __forceinline__ bool is_link(uint32_t s) { return slot_kind(s) == K_SPECIAL && slot_val(s) != V_INVALID; }
 
@@ -67,18 +94,20 @@ enum : int { F_BLOCK = 1, F_FINISH = 5, F_TREES = 6 };   // zlib::Flush values t
 // 0 entry (state in), 1 block header, 2 table builds, 3 inflate_fast, 4 window
 // load, 5 match copies, 6 done() and state out, 7 whole call, 8 input
 // staging; counts: 9 copies, 10 fast-loop tokens, 11 output bytes, 12
-// stagings, 13 calls, 14 input bytes
+// stagings, 13 calls, 14 input bytes; inside inflate_fast: 15 bit refill +
+// literal/length lookup, 16 literal store, 17 length extra + distance decode,
+// 18 loop tail, 19 the cost of one lap (two clock reads)
 #ifndef BPMD_ZSTREAM_HOST
-__device__ unsigned long long g_zprof[16];
+__device__ unsigned long long g_zprof[24];
 #endif
 #if defined(BPMD_PROF) && !defined(BPMD_ZSTREAM_HOST)
 #define ZP_NOW() ((unsigned long long)__builtin_amdgcn_s_memtime())
 #define ZP_ADD(i, v) (zp[i] += (unsigned long long)(v))
-#define ZP_DECL unsigned long long zp[16] = {};
+#define ZP_DECL unsigned long long zp[24] = {};
 #define ZP_FLUSH() \
     do { \
         if (lane == 0) \
-            for (int i_ = 0; i_ < 16; ++i_) atomicAdd(&g_zprof[i_], zp[i_]); \
+            for (int i_ = 0; i_ < 24; ++i_) atomicAdd(&g_zprof[i_], zp[i_]); \
     } while (0)
 #else
 #define ZP_NOW() 0ull
@@ -271,8 +300,17 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
         int32_t err = 0;
         const unsigned long long zf = ZP_NOW();
         (void)zf;
+        unsigned long long zl = ZP_NOW();
+        (void)zl;
         do {
             ZP_ADD(10, 1);
+#ifdef BPMD_ZSTREAM_LAPS
+            { const unsigned long long a = ZP_NOW(), b = ZP_NOW(); ZP_ADD(19, b - a); }
+#define ZLAP(i) do { const unsigned long long n_ = ZP_NOW(); ZP_ADD(i, n_ - zl); zl = n_; } while (0)
+#else
+#define ZLAP(i) ((void)0)
+#endif
+            ZLAP(18);
             if (bn < 15) {
                 pull();
                 pull();
@@ -284,11 +322,13 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
             }
             drop(slot_bits(s));
             const uint32_t kind = slot_kind(s), val = slot_val(s);
+            ZLAP(15);
             if (kind == K_VAL) {
                 put(val);
+                ZLAP(16);
             } else if (kind == K_LEN) {
-                uint32_t len = kLenBase[val];
-                const uint32_t x = kLenExtra[val];
+                uint32_t len = len_base(val);
+                const uint32_t x = len_extra(val);
                 if (x) {
                     if (bn < x) pull();
                     len += bv & ((1u << x) - 1u);
@@ -308,14 +348,15 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
                     err = ST_INVALID_DISTANCE_CODE;
                     break;
                 }
-                uint32_t dist = kDistBase[slot_val(d)];
-                const uint32_t dx = kDistExtra[slot_val(d)];
+                uint32_t dist = dist_base(slot_val(d));
+                const uint32_t dx = dist_extra(slot_val(d));
                 if (bn < dx) {
                     pull();
                     if (bn < dx) pull();
                 }
                 dist += bv & ((1u << dx) - 1u);
                 drop(dx);
+                ZLAP(17);
                 if (dist > op) {   // from the window
                     const uint64_t back = dist - op;
                     if (back > h.wsize) {
@@ -327,6 +368,7 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
                     len -= n;
                 }
                 if (len) copy_back(dist, len);   // from this call's output (room >= 258 here)
+                ZLAP(20);
             } else if (kind == K_EOB) {
                 h.mode = TYPE;
                 break;
@@ -565,8 +607,8 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
                 h.mode = BAD;
                 goto quiet;
             }
-            h.length = kLenBase[val];
-            h.extra = kLenExtra[val];
+            h.length = len_base(val);
+            h.extra = len_extra(val);
             h.mode = LENEXT;
         }
             [[fallthrough]];
@@ -594,8 +636,8 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
                 h.mode = BAD;
                 goto quiet;
             }
-            h.offset = kDistBase[slot_val(d)];
-            h.extra = kDistExtra[slot_val(d)];
+            h.offset = dist_base(slot_val(d));
+            h.extra = dist_extra(slot_val(d));
             h.mode = DISTEXT;
         }
             [[fallthrough]];
@@ -712,10 +754,10 @@ extern "C" int bpmd_internal_zstream_write(void* st, const uint8_t* in, uint64_t
 // diagnostic counters (meaningful only in the -DBPMD_PROF build)
 extern "C" int bpmd_diag_zstream_counters(unsigned long long* out, int reset)
 {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(bpmd::zst::g_zprof), sizeof(unsigned long long) * 16) != hipSuccess)
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(bpmd::zst::g_zprof), sizeof(unsigned long long) * 24) != hipSuccess)
         return -1;
     if (reset) {
-        unsigned long long z[16] = {0};
+        unsigned long long z[24] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(bpmd::zst::g_zprof), z, sizeof z) != hipSuccess) return -1;
     }
     return 0;

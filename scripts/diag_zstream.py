@@ -21,13 +21,14 @@ COUNTS = ["copies", "fast tokens", "output bytes", "stagings", "calls", "input b
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 128
+    size = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
     L = S._lib()
     L.bpmd_diag_zstream_counters.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
     zo, zi = S._mk(L, True, 8), S._mk(L, False)
-    data, off, ln = synth.make_batch("json", [1024] * n, seed=0x5EED0001)
-    msgs = [bytes(data[int(off[i]):int(off[i]) + 1024]) for i in range(n)]
+    data, off, ln = synth.make_batch("json", [size] * n, seed=0x5EED0001)
+    msgs = [bytes(data[int(off[i]):int(off[i]) + size]) for i in range(n)]
     L.bpmd_diag_deflate_counters.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    c = (ctypes.c_ulonglong * 16)()
+    c = (ctypes.c_ulonglong * 24)()
     dc = (ctypes.c_ulonglong * 24)()
     for i, m in enumerate(msgs):
         if i == 8:
@@ -39,10 +40,16 @@ def main():
     L.bpmd_diag_deflate_counters(dc, 0)
     k = n - 8
     calls = max(1, c[13])
-    print(f"{k} messages, {c[13]} calls; per message: {c[14] / k:.0f} input bytes, {c[11] / k:.0f} output bytes, "
+    print(f"{k} messages of {size} B, {c[13]} calls; per message: {c[14] / k:.0f} input bytes, {c[11] / k:.0f} output bytes, "
           f"{c[10] / k:.0f} fast-loop tokens, {c[9] / k:.0f} match copies, {c[12] / k:.1f} input stagings")
     for i, nm in enumerate(NAMES):
         print(f"  {nm:18s} {c[i] / k:10.0f} cycles per message ({c[i] / calls:9.0f} per call)")
+    if c[19]:   # the laps build (-DBPMD_ZSTREAM_LAPS): inside inflate_fast, per token
+        lap = c[19] / max(1, c[10])
+        print(f"  laps build, cycles per fast-loop token (one lap = {lap:.0f}, not subtracted):")
+        for i, nm in ((15, "refill + lookup"), (16, "literal store"), (17, "length + distance decode"),
+                      (20, "match copies"), (18, "loop tail")):
+            print(f"    {nm:26s} {c[i] / max(1, c[10]):8.0f}")
     if c[9]:
         print(f"  cycles per match copy {c[5] / c[9]:.0f}; per fast-loop token {c[3] / max(1, c[10]):.0f}")
     print("deflate (chunk kernel phases, per message):")

@@ -1,0 +1,13 @@
+#!/bin/bash
+# per-stream inflater: closed-form length/distance tables (TAG names the files)
+set -o pipefail
+TAG=${TAG:-r05p}
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_zstream.py tests/test_gpu_stream.py -x -q --timeout 120 --timeout-method thread > gpurun_out/${TAG}_pytest_zstream.log 2>&1 || { tail -30 gpurun_out/${TAG}_pytest_zstream.log; exit 1; }
+tail -1 gpurun_out/${TAG}_pytest_zstream.log
+BPMD_LIB=beast_amd/libbeast_pmd_prof.so timeout -k 10 300 python -u scripts/diag_zstream.py 72 > gpurun_out/${TAG}_diag_zstream.log 2>&1 || { tail -20 gpurun_out/${TAG}_diag_zstream.log; exit 2; }
+head -12 gpurun_out/${TAG}_diag_zstream.log
+timeout -k 10 300 python -u scripts/facade_latency.py > gpurun_out/${TAG}_facade_latency.log 2>&1 || { tail -20 gpurun_out/${TAG}_facade_latency.log; exit 3; }
+cat gpurun_out/${TAG}_facade_latency.log
+timeout -k 10 300 python -u -m pytest tests/test_facade.py -m gpu -k echo -q -s --timeout 280 --timeout-method thread > gpurun_out/${TAG}_c1_echo.log 2>&1 || { echo "c1 failed"; tail -20 gpurun_out/${TAG}_c1_echo.log; exit 4; }
+grep "C1 echo" gpurun_out/${TAG}_c1_echo.log
