@@ -52,6 +52,12 @@ constexpr unsigned CHUNK = 4096;
 constexpr unsigned HB = 11;
 constexpr unsigned HSIZE = 1u << HB;
 constexpr unsigned MIN_SEG = 32;
+// A lane whose finds have walked more than BPMD_CHAIN_BUDGET chain candidates
+// per 64 bytes of its parse segment walks at most 4 per find from then on
+// (0 = no budget): the busiest lane sets a chunk's parse time
+#ifndef BPMD_CHAIN_BUDGET
+#define BPMD_CHAIN_BUDGET 0
+#endif
 constexpr uint32_t NONE = 0xFFFFu;
 constexpr unsigned NODES = 576 + 64;          // lit tree nodes [0, 576), dist tree [576, 640)
 constexpr unsigned NODES_PER_LANE = NODES / WAVE;
@@ -919,6 +925,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
             const bool lazy = (pflags & 1u) != 0, no_match = (pflags & 2u) != 0, rle = (pflags & 4u) != 0,
                        filtered = (pflags & 8u) != 0;
             unsigned p = a, l0 = 0, d0 = 0;
+            const unsigned budget = BPMD_CHAIN_BUDGET ? to_vgpr((BPMD_CHAIN_BUDGET * seg + 63) / 64) : ~0u;
             bool have0 = false;
             bool mt = false;   // match state (chain otherwise)
             unsigned q = p, thr = MIN_MATCH - 1, c = 0, chain_left = 0, best = thr, bd = 0, nice = 0, maxl = 0,
@@ -932,6 +939,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
                 c = rle ? (q > 0 ? q - 1 : NONE) : h;
                 c = (no_match || q + MIN_MATCH > wn) ? NONE : c;
                 chain_left = rle ? 1u : (thr >= good ? chain_max >> 2 : chain_max);
+                if (BPMD_CHAIN_BUDGET) chain_left = steps > budget && chain_left > 4u ? 4u : chain_left;
                 nice = rle ? maxl : (nice_l < maxl ? nice_l : maxl);
             };
             setup();

@@ -36,6 +36,8 @@
 #include "huff_table.h"
 #include "huff_wave.h"
 #include "wave_util.h"
+#include <atomic>
+#include <cstdlib>
 #endif
 #include "zstream.h"
 
@@ -45,6 +47,14 @@ namespace zst {
 constexpr uint32_t HR = 65536, HM = HR - 1;   // history ring: window + this call's output
 constexpr uint32_t IST = 4096;               // input staging
 constexpr uint64_t FLUSH_AT = 16384;          // unflushed output kept below this (ring room)
+// wave-parallel inflate_fast (pfast): ZQ candidate bit offsets per lane per
+// window, a window's accepted output bounded by ZWOUT (+ one match), its
+// token-start bitmap ZBM words, input staged ZSPAN bytes past the window start
+constexpr uint32_t ZQ = 4, ZWOUT = 8192, ZSPAN = 64;
+constexpr uint32_t ZBM = (ZWOUT + 258 + 2 * 64) / 32 + 4;
+// pfast is used while at least this much input / output room is left (the
+// serial loop takes the last few tokens; both stop where inflate_fast stops)
+constexpr uint64_t ZMIN_IN = 24, ZMIN_OUT = 512;
 
 struct alignas(16) Lds {
     uint8_t hist[HR];
@@ -53,7 +63,27 @@ struct alignas(16) Lds {
     uint8_t lens[kLens];
     uint8_t flens[288];   // fixed-block code lengths (fixedTables, inflate_stream.ipp:865-930)
     WaveTableScratch ts;
+    uint32_t ptok[ZQ * WAVE];   // pfast: a window's accepted tokens, (olen << 16) | literal or distance
+    uint32_t pbm[ZBM];          // pfast: their first output byte, one bit per output byte of the window
 };
+
+// cross-lane steps of pfast (one-lane meanings in the host build)
+#ifndef BPMD_ZSTREAM_HOST
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t j) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j); }
+__device__ __forceinline__ uint64_t ballot64(bool p) { return __ballot(p); }
+__device__ __forceinline__ uint32_t shfl32(uint32_t v, uint32_t from) { return (uint32_t)__shfl((int)v, (int)from); }
+__device__ __forceinline__ uint32_t fsh(uint32_t hi, uint32_t lo, uint32_t sh) { return __builtin_amdgcn_alignbit(hi, lo, sh); }
+#else
+inline uint32_t rdlane(uint32_t v, uint32_t) { return v; }
+inline uint64_t ballot64(bool p) { return p ? 1u : 0u; }
+inline uint32_t shfl32(uint32_t v, uint32_t) { return v; }
+inline uint32_t fsh(uint32_t hi, uint32_t lo, uint32_t sh) { return (uint32_t)((((uint64_t)hi << 32) | lo) >> (sh & 31)); }
+inline void atomicOr(uint32_t* p, uint32_t v) { *p |= v; }
+#endif
+// a candidate token: A = c1 | x << 4 | c2 << 7 | dx << 11 | kind << 15 (bits of
+// the literal/length code incl. a sub-table's, length extra, distance code,
+// distance extra); B = (output bytes << 16) | literal or distance
+enum : uint32_t { Z_LIT = 0, Z_MATCH = 1, Z_EOB = 2, Z_BADLIT = 3, Z_BADDIST = 4 };
 
 // RFC 1951 §3.2.5's length and distance bases and extra bits in closed form,
 // equal to the tables at every value a K_LEN slot (0..28) or a distance K_VAL
@@ -117,7 +147,7 @@ __device__ unsigned long long g_zprof[24];
 #endif
 
 __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __restrict__ in, uint64_t n_in,
-                            uint8_t* __restrict__ out, uint64_t cap, int flush, Result* __restrict__ res)
+                            uint8_t* __restrict__ out, uint64_t cap, int flush, Result* __restrict__ res, int par)
 {
     const unsigned lane = lane_id();
     ZP_DECL
@@ -368,7 +398,7 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
                     len -= n;
                 }
                 if (len) copy_back(dist, len);   // from this call's output (room >= 258 here)
-                ZLAP(20);
+                ZLAP(23);
             } else if (kind == K_EOB) {
                 h.mode = TYPE;
                 break;
@@ -381,6 +411,231 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
         if (err) h.mode = BAD;
         rewind();
         ZP_ADD(3, ZP_NOW() - zf);
+        return err;
+    };
+
+    // ---- inflate_fast, wave-parallel.  Per window of ZQ * WAVE bit offsets from
+    // the next token's first bit, every lane decodes the token that would start
+    // at each of its ZQ offsets (a token's symbols are a function of the bits:
+    // every lookup of fast() sees >= 15 valid bits); the scalar unit follows
+    // the chain of real token starts through those candidates and replays
+    // fast() on it token by token -- its byte refills (so ip and bn are
+    // fast()'s), its checks in fast()'s order and its loop condition -- and
+    // the lanes then write the accepted tokens' bytes 64 at a time (a match
+    // reaching into the same 64 bytes by pointer jumping).  So the tokens, the
+    // stopping point, ip / bv / bn and the error are fast()'s.
+    auto pfast = [&]() -> int32_t {
+        const uint64_t in_last = n_in - 5, out_last = cap - 257;
+        const uint32_t lroot = h.lroot, droot = h.droot, dtab = h.dtab;
+        const uint32_t lmask = (1u << lroot) - 1u, dmask = (1u << droot) - 1u;
+        const uint64_t wsize = h.wsize;
+        const uint32_t* iw = (const uint32_t*)L.ist;
+        int32_t err = 0;
+        bool stop = false;
+        const unsigned long long zp0 = ZP_NOW();
+        unsigned long long zq = zp0;
+        (void)zp0;
+        (void)zq;
+        int64_t sb = 0;   // L.ist[i] holds input byte sb + i
+        bool virt = false;
+        while (!stop) {
+            if (bn > ip * 8) {
+                if (virt) goto staged;   // (bv is the reservoir only on entry)
+                // the reservoir still holds bits of an earlier call's input: a
+                // window of its own, L.ist = the bn bits (padded in front to a
+                // byte) followed by this call's input from ip on
+                const uint32_t nb = (bn + 7) >> 3, k = 8 * nb - bn;
+                const uint64_t pre = (uint64_t)bv << k;
+                wave_sync();
+                for (uint32_t i = lane; i < ZSPAN + 16; i += WAVE)
+                    L.ist[i] = i < nb ? (uint8_t)(pre >> (8 * i)) : (ip + i - nb < n_in ? in[ip + i - nb] : (uint8_t)0);
+                wave_sync();
+                sb = (int64_t)ip - (int64_t)nb;
+                ib0 = ib1 = ~0ull >> 1;   // the staging pull() uses is gone
+                virt = true;
+            } else {
+                const uint64_t P = ip * 8 - bn;   // the next token's first bit
+                if ((P >> 3) < ib0 || (P >> 3) >= ib1 || (P >> 3) + ZSPAN > ib0 + IST) stage(P >> 3);
+                sb = (int64_t)ib0;
+            }
+        staged:
+            const uint32_t rb = (uint32_t)((int64_t)(ip * 8) - (int64_t)bn - 8 * sb);
+            ZP_ADD(15, ZP_NOW() - zq);
+            zq = ZP_NOW();
+            // candidates at bits rb + lane + WAVE q of the staged input
+            uint32_t ca[ZQ], cb[ZQ];
+#pragma unroll
+            for (uint32_t q = 0; q < ZQ; ++q) {
+                const uint32_t r = rb + lane + WAVE * q, w = r >> 5, sh = r & 31;
+                const uint32_t d0 = iw[w], d1 = iw[w + 1], d2 = iw[w + 2];
+                const uint64_t v = ((uint64_t)fsh(d2, d1, sh) << 32) | fsh(d1, d0, sh);
+                uint32_t sl = L.tab[(uint32_t)v & lmask], c1;
+                if (is_link(sl)) {
+                    sl = L.tab[slot_val(sl) + ((uint32_t)(v >> lroot) & ((1u << slot_bits(sl)) - 1u))];
+                    c1 = lroot + slot_bits(sl);
+                } else {
+                    c1 = slot_bits(sl);
+                }
+                const uint32_t kind = slot_kind(sl), val = slot_val(sl);
+                uint32_t a = c1 | (kind == K_VAL ? Z_LIT : kind == K_EOB ? Z_EOB : Z_BADLIT) << 15, b = (1u << 16) | val;
+                if (kind == K_LEN) {
+                    const uint32_t x = len_extra(val);
+                    const uint32_t len = len_base(val) + ((uint32_t)(v >> c1) & ((1u << x) - 1u));
+                    const uint32_t u = c1 + x;
+                    uint32_t d = L.tab[dtab + ((uint32_t)(v >> u) & dmask)], c2;
+                    if (is_link(d)) {
+                        d = L.tab[dtab + slot_val(d) + ((uint32_t)(v >> (u + droot)) & ((1u << slot_bits(d)) - 1u))];
+                        c2 = droot + slot_bits(d);
+                    } else {
+                        c2 = slot_bits(d);
+                    }
+                    if (slot_kind(d) != K_VAL) {
+                        a = c1 | x << 4 | c2 << 7 | Z_BADDIST << 15;
+                    } else {
+                        const uint32_t dx = dist_extra(slot_val(d));
+                        const uint32_t dist = dist_base(slot_val(d)) + ((uint32_t)(v >> (u + c2)) & ((1u << dx) - 1u));
+                        a = c1 | x << 4 | c2 << 7 | dx << 11 | Z_MATCH << 15;
+                        b = (len << 16) | dist;
+                    }
+                }
+                ca[q] = a;
+                cb[q] = b;
+            }
+            for (uint32_t i = lane; i < ZBM; i += WAVE) L.pbm[i] = 0;
+            wave_sync();
+            ZP_ADD(16, ZP_NOW() - zq);
+            zq = ZP_NOW();
+            // the chain, replaying fast() (inflate_stream.ipp:979-1113)
+            const uint64_t op0 = op;
+            uint32_t o = 0, acc = 0, wout = 0;
+            bool needwin = false;
+#pragma unroll
+            for (uint32_t q = 0; q < ZQ; ++q) {
+                while (!stop && o < WAVE * (q + 1) && wout < ZWOUT) {
+                    const uint32_t a = rdlane(ca[q], o - WAVE * q);
+                    const uint32_t c1 = a & 15u, x = (a >> 4) & 7u, c2 = (a >> 7) & 15u, dx = (a >> 11) & 15u,
+                                   kind = a >> 15;
+                    if (bn < 15) {   // pull(); pull();
+                        ip += 2;
+                        bn += 16;
+                    }
+                    bn -= c1;
+                    if (kind == Z_EOB) {
+                        h.mode = TYPE;
+                        stop = true;
+                        break;
+                    }
+                    if (kind == Z_BADLIT) {
+                        err = ST_INVALID_LITERAL_LENGTH;
+                        stop = true;
+                        break;
+                    }
+                    const uint32_t b = rdlane(cb[q], o - WAVE * q);
+                    if (kind != Z_LIT) {
+                        if (x) {
+                            if (bn < x) {
+                                ip += 1;
+                                bn += 8;
+                            }
+                            bn -= x;
+                        }
+                        if (bn < 15) {
+                            ip += 2;
+                            bn += 16;
+                        }
+                        bn -= c2;
+                        if (kind == Z_BADDIST) {
+                            err = ST_INVALID_DISTANCE_CODE;
+                            stop = true;
+                            break;
+                        }
+                        if (bn < dx) {
+                            ip += 1;
+                            bn += 8;
+                            if (bn < dx) {
+                                ip += 1;
+                                bn += 8;
+                            }
+                        }
+                        bn -= dx;
+                        const uint64_t dist = b & 0xffffu, opc = op0 + wout;
+                        if (dist > opc) {   // from the window
+                            if (dist - opc > wsize) {
+                                err = ST_INVALID_DISTANCE;
+                                stop = true;
+                                break;
+                            }
+                            needwin = true;
+                        }
+                    }
+                    if (lane == 0) {
+                        L.ptok[acc] = b;
+                        atomicOr(&L.pbm[wout >> 5], 1u << (wout & 31));
+                    }
+                    ++acc;
+                    wout += b >> 16;
+                    o += c1 + x + c2 + dx;
+                    if (!(ip < in_last && op0 + wout < out_last)) stop = true;
+                }
+            }
+            ZP_ADD(21, 1);
+            ZP_ADD(22, acc);
+            ZP_ADD(17, ZP_NOW() - zq);
+            zq = ZP_NOW();
+            // the accepted tokens' bytes
+            if (needwin && !winld) load_window();
+            wave_sync();
+            {
+                int32_t tprev = -1;
+                const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+                const uint64_t wmask = WAVE == 64 ? ~0ull : ((1ull << WAVE) - 1);
+                for (uint32_t c = 0; c < wout; c += WAVE) {
+                    const uint32_t w = c >> 5, sh = c & 31;
+                    const uint64_t lo = L.pbm[w] | ((uint64_t)L.pbm[w + 1] << 32);
+                    const uint64_t B = (sh ? (lo >> sh) | ((uint64_t)L.pbm[w + 2] << (64 - sh)) : lo) & wmask;
+                    const uint32_t rel = c + lane;
+                    const bool act = rel < wout;
+                    const int32_t T = tprev + (int32_t)__builtin_popcountll(B & upto);
+                    const uint32_t info = act ? L.ptok[T] : (1u << 16);
+                    uint32_t val = info & 0xffu;
+                    int32_t src = (int32_t)rel - (int32_t)(info & 0xffffu);   // relative to op0
+                    bool pend = false;
+                    if (act && (info >> 16) >= 3) {
+                        if (src >= (int32_t)c) pend = true;
+                        else val = L.hist[((uint32_t)op0 + (uint32_t)src) & HM];
+                    }
+                    while (ballot64(pend)) {   // a match reaching into these bytes
+                        const uint32_t from = pend ? (uint32_t)src - c : lane;
+                        const uint32_t v2 = shfl32(val, from);
+                        const int32_t s2 = (int32_t)shfl32((uint32_t)src, from);
+                        const bool p2 = shfl32(pend ? 1u : 0u, from) != 0;
+                        if (pend) {
+                            if (!p2) {
+                                val = v2;
+                                pend = false;
+                            } else {
+                                src = s2;
+                            }
+                        }
+                    }
+                    if (act) L.hist[((uint32_t)op0 + rel) & HM] = (uint8_t)val;
+                    tprev += (int32_t)__builtin_popcountll(B);
+                    wave_sync();
+                }
+            }
+            op = op0 + wout;
+            if (op - flushed >= FLUSH_AT) flush_out();
+            ZP_ADD(18, ZP_NOW() - zq);
+            zq = ZP_NOW();
+        }
+        // fast()'s reservoir holds the bn stream bits before ip
+        pfip = ~0ull;
+        pfn = 0;
+        if (err) h.mode = BAD;
+        ip -= bn >> 3;   // rewind()
+        bn &= 7;
+        bv = bn ? uni((uint32_t)L.ist[(uint32_t)((int64_t)ip - 1 - sb)]) >> (8 - bn) : 0u;
+        ZP_ADD(20, ZP_NOW() - zp0);
         return err;
     };
 
@@ -575,7 +830,7 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
             [[fallthrough]];
         case LEN: {
             if (n_in - ip >= 6 && cap - op >= 258) {
-                const int32_t e = fast();
+                const int32_t e = par && n_in - ip >= ZMIN_IN && cap - op >= ZMIN_OUT ? pfast() : fast();
                 if (e) {
                     ec = e;
                     goto quiet;
@@ -729,10 +984,10 @@ quiet:
 #ifndef BPMD_ZSTREAM_HOST
 __global__ void __launch_bounds__(WAVE)
 zstream_write_kernel(State* __restrict__ st, const uint8_t* __restrict__ in, uint64_t n_in, uint8_t* __restrict__ out,
-                     uint64_t cap, int flush, Result* __restrict__ res)
+                     uint64_t cap, int flush, Result* __restrict__ res, int par)
 {
     __shared__ Lds L;
-    zstream_run(L, st, in, n_in, out, cap, flush, res);
+    zstream_run(L, st, in, n_in, out, cap, flush, res, par);
 }
 #endif
 
@@ -742,12 +997,28 @@ zstream_write_kernel(State* __restrict__ st, const uint8_t* __restrict__ in, uin
 #ifndef BPMD_ZSTREAM_HOST
 // One inflate_stream::write() on `stream`: st is the stream's device state,
 // in/out device buffers of n_in bytes and `cap` bytes of room.
+// BPMD_ZSTREAM_PAR=0 (or bpmd_diag_set_zstream_parallel(0)): the serial
+// inflate_fast loop instead of the wave-parallel one (same results)
+static std::atomic<int> g_zst_par{-1};
+
+extern "C" int bpmd_diag_set_zstream_parallel(int on)
+{
+    g_zst_par.store(on < 0 ? -1 : (on ? 1 : 0));
+    return 0;
+}
+
 extern "C" int bpmd_internal_zstream_write(void* st, const uint8_t* in, uint64_t n_in, uint8_t* out, uint64_t cap,
                                            int flush, void* res, hipStream_t stream)
 {
     using namespace bpmd::zst;
+    static const int env_par = [] {
+        const char* e = getenv("BPMD_ZSTREAM_PAR");
+        return e ? (atoi(e) ? 1 : 0) : 1;
+    }();
+    const int o = g_zst_par.load();
+    const int par = o < 0 ? env_par : o;
     hipLaunchKernelGGL(zstream_write_kernel, dim3(1), dim3(bpmd::WAVE), 0, stream, (State*)st, in, n_in, out, cap,
-                       flush, (Result*)res);
+                       flush, (Result*)res, par);
     return (int)hipGetLastError();
 }
 

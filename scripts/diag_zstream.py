@@ -44,11 +44,16 @@ def main():
           f"{c[10] / k:.0f} fast-loop tokens, {c[9] / k:.0f} match copies, {c[12] / k:.1f} input stagings")
     for i, nm in enumerate(NAMES):
         print(f"  {nm:18s} {c[i] / k:10.0f} cycles per message ({c[i] / calls:9.0f} per call)")
+    if c[21]:   # the wave-parallel inflate_fast
+        print(f"  pfast: {c[21] / k:.1f} windows and {c[22] / k:.0f} tokens per message, {c[20] / k:.0f} cycles "
+              f"({c[20] / max(1, c[22]):.0f} per token): staging {c[15] / k:.0f}, candidates {c[16] / k:.0f}, "
+              f"chain {c[17] / k:.0f}, output {c[18] / k:.0f}")
+        print(f"  outside inflate_fast and the header: {(c[7] - c[20] - c[3] - c[1] - c[0] - c[6]) / k:.0f} cycles per message")
     if c[19]:   # the laps build (-DBPMD_ZSTREAM_LAPS): inside inflate_fast, per token
         lap = c[19] / max(1, c[10])
         print(f"  laps build, cycles per fast-loop token (one lap = {lap:.0f}, not subtracted):")
         for i, nm in ((15, "refill + lookup"), (16, "literal store"), (17, "length + distance decode"),
-                      (20, "match copies"), (18, "loop tail")):
+                      (23, "match copies"), (18, "loop tail")):
             print(f"    {nm:26s} {c[i] / max(1, c[10]):8.0f}")
     if c[9]:
         print(f"  cycles per match copy {c[5] / c[9]:.0f}; per fast-loop token {c[3] / max(1, c[10]):.0f}")

@@ -18,6 +18,13 @@ from tests import test_gpu_stream as S  # noqa: E402
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+    busy = os.environ.get("BPMD_LAT_BUSY")   # a spin kernel on a side stream meanwhile (clock ramp check)
+    if busy:
+        import torch
+        side = torch.cuda.Stream()
+        with torch.cuda.stream(side):
+            for _ in range(int(busy)):
+                torch.cuda._sleep(1 << 30)
     L = S._lib()
     zo, zi = S._mk(L, True, 8), S._mk(L, False)
     data, off, ln = synth.make_batch("json", [1024] * n, seed=0x5EED0001)
@@ -34,7 +41,7 @@ def main():
             td += t1 - t0
             ti += t2 - t1
     k = n - 8
-    print(f"facade per message: deflate {td / k * 1e6:.1f} us, inflate {ti / k * 1e6:.1f} us "
+    print(f"{'busy ' if busy else ''}facade per message: deflate {td / k * 1e6:.1f} us, inflate {ti / k * 1e6:.1f} us "
           f"(ws_deflate_message: none/block/sync writes; ws_inflate_message: rd_buf slices + the 4-byte tail)")
     L.bpmd_stream_destroy(zo)
     L.bpmd_stream_destroy(zi)

@@ -30,6 +30,8 @@ SHIM_TEXT = r"""
 #include <stdint.h>
 #include <stddef.h>
 #include <string.h>
+#include <stdlib.h>
+#include <stdio.h>
 #define __device__
 #define __host__
 #define __forceinline__ inline
@@ -90,7 +92,10 @@ extern "C" int zs_host_write(void* st, const uint8_t* in, uint64_t n, uint8_t* o
                              void* res)
 {
     static thread_local bpmd::zst::Lds L;
-    bpmd::zst::zstream_run(L, (bpmd::zst::State*)st, in, n, out, cap, flush, (bpmd::zst::Result*)res);
+    // BPMD_ZSTREAM_PAR=0: the serial inflate_fast loop (default: the parallel one, one lane)
+    const char* e = getenv("BPMD_ZSTREAM_PAR");
+    const int par = e ? atoi(e) != 0 : 1;
+    bpmd::zst::zstream_run(L, (bpmd::zst::State*)st, in, n, out, cap, flush, (bpmd::zst::Result*)res, par);
     return ((bpmd::zst::Result*)res)->ec;
 }
 """
@@ -105,7 +110,7 @@ def build():
         f.write(SHIM_TEXT)
     with open(GEN, "w") as f:
         f.write('#include "pmd_zstream.hip"\n' + DRIVER)
-    cmd = [CXX, "-O1", "-g", "-std=c++17", "-fPIC", "-shared", "-DBPMD_ZSTREAM_HOST", "-x", "c++",
+    cmd = [CXX, "-O1", "-g", *os.environ.get("ZS_HOST_FLAGS", "").split(), "-std=c++17", "-fPIC", "-shared", "-DBPMD_ZSTREAM_HOST", "-x", "c++",
            "-include", SHIM, "-I", CSRC, "-o", LIB, GEN]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:

@@ -114,6 +114,26 @@ def test_errors_then_bad_mode():
     Z.case_errors(make)
 
 
+@pytest.mark.parametrize("par", [0, 1])
+def test_serial_and_parallel_fast_loops(par):
+    """inflate_fast runs wave-parallel by default (pmd_zstream.hip pfast: the
+    lanes decode every candidate bit offset of a window, the scalar unit
+    replays inflate_fast on the chain of real token starts); the serial loop
+    it replays stays selectable (bpmd_diag_set_zstream_parallel /
+    BPMD_ZSTREAM_PAR=0).  Both must give the oracle's write()s."""
+    L = _lib()
+    L.bpmd_diag_set_zstream_parallel.argtypes = [ctypes.c_int]
+    L.bpmd_diag_set_zstream_parallel(par)
+    try:
+        for kind in ("json", "binary", "random"):
+            Z.case_connection_random_cuts(make, kind, 6, 4)
+        Z.case_foreign_payloads(make)
+        Z.case_errors(make)
+        Z.case_small_window(make)
+    finally:
+        L.bpmd_diag_set_zstream_parallel(-1)
+
+
 def test_reset_between_streams():
     """reset(windowBits) mid-stream: fresh state and window, new size."""
     msgs = Z.msgs_of("json", [5000, 5000], seed=31)
