@@ -131,6 +131,24 @@ LZ_HD uint32_t reverse_bits(uint32_t code, unsigned len)
 // matches than Beast's 128-candidate one on 3-byte chains, and 3-byte matches
 // (worth 1-2 bits each) are found only at a window's end.  C3 at level 6:
 // 33.1 -> 34.4 GiB/s, 1.020 -> 0.991x Beast's size.
+// Incompressible chunks (round 5).  After the chains are built, every
+// INCOMP_STRIDE-th position q of the chunk (q + 4 within the window) counts a
+// hit when the head of its chain holds the same 4 bytes.  With fewer than one
+// hit per INCOMP_DEN chunk bytes (sampled: hits * INCOMP_STRIDE * INCOMP_DEN <
+// chunk bytes) the
+// chunk is near-random and the parse would find almost no matches, so it is
+// coded as literals without one (a dynamic or stored block as usual); 0 turns
+// the test off.  Beast has no such test; the size change on C5's near-random
+// bytes is in DESIGN.md 4.2.
+#ifndef BPMD_INCOMP_DEN
+#define BPMD_INCOMP_DEN 64
+#endif
+constexpr unsigned INCOMP_DEN = BPMD_INCOMP_DEN, INCOMP_STRIDE = 4;
+LZ_HD bool incompressible(unsigned hits, unsigned chunk_bytes)
+{
+    return INCOMP_DEN && (unsigned long long)hits * INCOMP_STRIDE * INCOMP_DEN < chunk_bytes;
+}
+
 LZ_HD uint32_t chain_hash(uint32_t w, unsigned avail, unsigned hbits)
 {
 #ifdef BPMD_CHAIN_KEY3   // diagnostics: round 2's 3-byte keys

@@ -58,6 +58,9 @@ constexpr unsigned MIN_SEG = 32;
 #ifndef BPMD_CHAIN_BUDGET
 #define BPMD_CHAIN_BUDGET 0
 #endif
+// lz::INCOMP_DEN (lz_core.h): a chunk whose sampled positions almost never
+// repeat their 4-byte key at the head of their chain is coded as literals
+// without the parse
 constexpr uint32_t NONE = 0xFFFFu;
 constexpr unsigned NODES = 576 + 64;          // lit tree nodes [0, 576), dist tree [576, 640)
 constexpr unsigned NODES_PER_LANE = NODES / WAVE;
@@ -887,6 +890,23 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
 #endif
         }
         wave_sync();
+        // incompressible chunk (near-random bytes): every INCOMP_STRIDE-th
+        // position of the chunk, is the head of its chain the same 4 bytes?
+        // Under one in INCOMP_DEN, the parse would find almost nothing: all
+        // literals.  64 samples per step; a chunk with repeats (JSON) has
+        // passed the threshold after the first step and stops there.
+        bool no_parse = false;
+        if (INCOMP_DEN && chains) {
+            unsigned hits = 0;
+            no_parse = true;
+            for (unsigned g = a0; g + 4 <= wn && no_parse; g += INCOMP_STRIDE * WAVE) {
+                const unsigned q = g + INCOMP_STRIDE * lane;
+                const uint32_t c = q + 4 <= wn ? S.a.prev[q] : NONE;
+                const bool hit = c != NONE && W.dw(c) == W.dw(q);
+                hits += (unsigned)__builtin_popcountll(__ballot(hit));
+                no_parse = incompressible(hits, clen);
+            }
+        }
         pf.lap(1);
         [[maybe_unused]] unsigned steps = 0, finds = 0, iters = 0;
         // ---- parse (head table dead from here; tok[] reuses it)
@@ -907,7 +927,10 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
             for (unsigned i = lane; i < CHUNK * 2 / 16; i += WAVE) t4[i] = make_uint4(0, 0, 0, 0);
         }
         wave_sync();
-        if (active) {
+        if (active && no_parse) {
+            own_end = b;
+            bm = b - a >= 64 ? ~0ull : (1ull << (b - a)) - 1;
+        } else if (active) {
             // The reference's parse loop (f_fast / f_slow) and longest_match
             // chain walk, flattened into one state machine so that every
             // iteration does one unit of work per lane (one chain candidate,

@@ -170,6 +170,14 @@ static std::vector<uint8_t> encode(const uint8_t* msg, unsigned n, const Params&
                 prev[q] = head[h];
                 head[h] = (int32_t)q;
             }
+            // incompressible chunk: all literals, no parse (lz_core.h incompressible)
+            bool no_parse = false;
+            if (INCOMP_DEN && P.strategy != 2 && P.strategy != 3) {
+                unsigned hits = 0;
+                for (unsigned q = a0; q + 4 <= wn; q += INCOMP_STRIDE)
+                    hits += prev[q] >= 0 && memcmp(w + prev[q], w + q, 4) == 0;
+                no_parse = incompressible(hits, wn - a0);
+            }
             unsigned len = wn - a0;
             unsigned seg = (len + P.lanes - 1) / P.lanes;
             if (seg < (unsigned)P.min_seg) seg = P.min_seg;
@@ -177,7 +185,10 @@ static std::vector<uint8_t> encode(const uint8_t* msg, unsigned n, const Params&
             for (unsigned s = a0; s < wn; s += seg) {
                 unsigned b = s + seg < wn ? s + seg : wn;
                 std::vector<Tok> lt;
-                parse_segment(w, prev.data(), s, b, wn, Q, L, max_dist, lt);
+                if (no_parse)
+                    for (unsigned q = s; q < b; ++q) lt.push_back({q, 1, 0});
+                else
+                    parse_segment(w, prev.data(), s, b, wn, Q, L, max_dist, lt);
                 // boundary repair against the previous segments' end E
                 for (const Tok& t : lt) {
                     if (t.pos + t.len <= E) continue;

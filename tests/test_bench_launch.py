@@ -43,8 +43,10 @@ dist.init_process_group("gloo")
 import torch
 t = torch.tensor([int(os.environ["RANK"])])
 dist.all_reduce(t)
-print(json.dumps({"rank": int(os.environ["RANK"]), "world": int(os.environ["WORLD_SIZE"]),
-                  "sum": int(t), "argv": sys.argv[1:]}), flush=True)
+# one file per rank: the ranks share the launcher's stdout, whose lines can interleave
+with open(os.path.join(os.environ["PROBE_DIR"], "rank%s.json" % os.environ["RANK"]), "w") as f:
+    json.dump({"rank": int(os.environ["RANK"]), "world": int(os.environ["WORLD_SIZE"]),
+               "sum": int(t), "argv": sys.argv[1:]}, f)
 dist.destroy_process_group()
 """
 
@@ -53,9 +55,10 @@ def test_launcher_starts_two_gloo_ranks(tmp_path, monkeypatch):
     probe = tmp_path / "probe.py"
     probe.write_text(PROBE)
     monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setenv("PROBE_DIR", str(tmp_path))
     cmd = bench.launch_cmd(["--gpus", "2"], 2, bench._free_port(), script=str(probe))
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stderr[-2000:]
-    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    lines = [json.load(open(tmp_path / f"rank{k}.json")) for k in range(2)]
     assert sorted(x["rank"] for x in lines) == [0, 1]
     assert all(x["world"] == 2 and x["sum"] == 1 and x["argv"] == ["--gpus", "2"] for x in lines)
