@@ -58,6 +58,14 @@ constexpr unsigned MIN_SEG = 32;
 #ifndef BPMD_CHAIN_BUDGET
 #define BPMD_CHAIN_BUDGET 0
 #endif
+// BPMD_DUAL_TEST: an iteration of the parse's chain walk that rejects its
+// candidate outright (no longer match, no byte run to extend) also tests the
+// next candidate of the chain, with the same limits and in the same order
+// (1), and in the chunk kernel (chain cap 32) a third after that (2; the
+// single-chunk kernel's walks are capped at 4 and lose with three)
+#ifndef BPMD_DUAL_TEST
+#define BPMD_DUAL_TEST 2
+#endif
 // lz::INCOMP_DEN (lz_core.h): a chunk whose sampled positions almost never
 // repeat their 4-byte key at the head of their chain is coded as literals
 // without the parse
@@ -952,7 +960,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
             bool have0 = false;
             bool mt = false;   // match state (chain otherwise)
             unsigned q = p, thr = MIN_MATCH - 1, c = 0, chain_left = 0, best = thr, bd = 0, nice = 0, maxl = 0,
-                     l = 0;
+                     l = 0, cn = NONE;   // cn: the candidate after c
             // find setup at q: chain head and limits; no candidate (c = NONE)
             // ends the find at the next iteration with best = thr
             auto setup = [&]() {
@@ -961,6 +969,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
                 asm volatile("" : "+v"(h));   // one load for every lane, not a branch on rle
                 c = rle ? (q > 0 ? q - 1 : NONE) : h;
                 c = (no_match || q + MIN_MATCH > wn) ? NONE : c;
+                if (BPMD_DUAL_TEST) cn = S.a.prev[c < wn ? c : 0];
                 chain_left = rle ? 1u : (thr >= good ? chain_max >> 2 : chain_max);
                 if (BPMD_CHAIN_BUDGET) chain_left = steps > budget && chain_left > 4u ? 4u : chain_left;
                 nice = rle ? maxl : (nice_l < maxl ? nice_l : maxl);
@@ -968,6 +977,65 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
             setup();
             while (p < b) {
                 ++iters;
+#if BPMD_DUAL_TEST
+                // every load issued up front: candidate c, the next one cn (its
+                // prev cnn, and cnn's prev for an iteration that uses both)
+                const unsigned cc = c < wn ? c : 0, cc2 = cn < wn ? cn : 0;
+                const uint32_t cnn = S.a.prev[cc2];
+                const uint32_t cb = W.byte(cc + best), qb = W.byte(q + best), cb2 = W.byte(cc2 + best);
+                const uint64_t cv = W.qw(cc + l), qv = W.qw(q + l), cv2 = W.qw(cc2);
+                const unsigned cc3 = cnn < wn ? cnn : 0;
+                const uint32_t cnnn = S.a.prev[cc3];
+                constexpr bool T3 = BPMD_DUAL_TEST > 1 && HIST > 0;   // (unused loads fold away without)
+                const uint32_t cb3 = T3 ? W.byte(cc3 + best) : 0u;
+                const uint64_t cv3 = T3 ? W.qw(cc3) : 0ull;
+                const uint32_t c4 = T3 ? S.a.prev[cnnn < wn ? cnnn : 0] : NONE;
+                const unsigned k3 = eq_bytes(cv3, qv);
+                const unsigned k = eq_bytes(cv, qv), k2 = eq_bytes(cv2, qv);   // qv = qw(q) outside a match
+                const bool ch = !mt;
+                // bitwise, not short-circuit: no branches
+                const bool term = ch & ((c == NONE) | (q - c > max_dist) | (chain_left == 0));
+                const bool test = ch & !term;
+                const bool quick = test & (best < maxl) & (cb == qb) & (k > 0);
+                const bool go_match = quick & (k == 8) & (maxl > 8);
+                const bool ext = mt & (k == 8) & (l + 8 < maxl);
+                const bool have_len = (quick & !go_match) | (mt & !ext);
+                const unsigned len = l + k < maxl ? l + k : maxl;
+                const bool improve = have_len & (len > best);
+                // c rejected with best unchanged: cn is tested as the next
+                // iteration would (same best, chain_left one lower)
+                const bool rej1 = test & !go_match & !improve;
+                const unsigned cl1 = chain_left - test;
+                const bool term2 = rej1 & ((cn == NONE) | (q - cn > max_dist) | (cl1 == 0));
+                const bool test2 = rej1 & !term2;
+                const bool quick2 = test2 & (best < maxl) & (cb2 == qb) & (k2 > 0);
+                const bool go2 = quick2 & (k2 == 8) & (maxl > 8);
+                const unsigned len2 = k2 < maxl ? k2 : maxl;
+                const bool improve2 = quick2 & !go2 & (len2 > best);
+                // and a third (cnn) when cn was rejected outright too
+                const bool rej2 = T3 & test2 & !go2 & !improve2;
+                const unsigned cl2 = cl1 - test2;
+                const bool term3 = rej2 & ((cnn == NONE) | (q - cnn > max_dist) | (cl2 == 0));
+                const bool test3 = rej2 & !term3;
+                const bool quick3 = test3 & (best < maxl) & (cb3 == qb) & (k3 > 0);
+                const bool go3 = quick3 & (k3 == 8) & (maxl > 8);
+                const unsigned len3 = k3 < maxl ? k3 : maxl;
+                const bool improve3 = quick3 & !go3 & (len3 > best);
+                best = improve ? len : improve2 ? len2 : improve3 ? len3 : best;
+                bd = improve ? q - c : improve2 ? q - cn : improve3 ? q - cnn : bd;
+                const bool found = term | (improve & (len >= nice)) | term2 | (improve2 & (len2 >= nice)) | term3 |
+                                   (improve3 & (len3 >= nice));
+                steps += test + test2 + test3;
+                chain_left = cl2 - test3;
+                const bool adv3 = rej2 & !found & !go3;               // c, cn, cnn done
+                const bool adv2 = rej1 & !rej2 & !found & !go2;       // c and cn done
+                const bool adv1 = !rej1 & !found & ((test & !go_match) | (mt & !ext));
+                l = go_match || go2 || go3 ? 8u : ext ? l + 8 : 0u;
+                const unsigned c_new = adv3 ? cnnn : (adv2 || go3) ? cnn : (adv1 || go2) ? cn : c;
+                cn = adv3 ? c4 : (adv2 || go3) ? cnnn : (adv1 || go2) ? cnn : cn;
+                c = c_new;
+                mt = go_match || ext || go2 || go3;
+#else
                 // every load issued up front
                 const unsigned cc = c < wn ? c : 0;
                 const uint32_t pn = S.a.prev[cc];
@@ -993,6 +1061,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
                 l = go_match ? 8u : ext ? l + 8 : 0u;
                 c = advance ? pn : c;
                 mt = go_match || ext;
+#endif
                 if (found) {
                     // f_slow / f_fast decision, as selects
                     const bool drop = best > thr && best <= 5 &&
