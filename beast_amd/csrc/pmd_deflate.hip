@@ -991,6 +991,12 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
                 const uint64_t cv3 = T3 ? W.qw(cc3) : 0ull;
                 const uint32_t c4 = T3 ? S.a.prev[cnnn < wn ? cnnn : 0] : NONE;
                 const unsigned k3 = eq_bytes(cv3, qv);
+                constexpr bool T4 = BPMD_DUAL_TEST > 2 && HIST > 0;
+                const unsigned cc4 = cnnn < wn ? cnnn : 0;
+                const uint32_t cb4 = T4 ? W.byte(cc4 + best) : 0u;
+                const uint64_t cv4 = T4 ? W.qw(cc4) : 0ull;
+                const uint32_t c5 = T4 ? S.a.prev[c4 < wn ? c4 : 0] : NONE;
+                const unsigned k4 = eq_bytes(cv4, qv);
                 const unsigned k = eq_bytes(cv, qv), k2 = eq_bytes(cv2, qv);   // qv = qw(q) outside a match
                 const bool ch = !mt;
                 // bitwise, not short-circuit: no branches
@@ -1021,20 +1027,29 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
                 const bool go3 = quick3 & (k3 == 8) & (maxl > 8);
                 const unsigned len3 = k3 < maxl ? k3 : maxl;
                 const bool improve3 = quick3 & !go3 & (len3 > best);
-                best = improve ? len : improve2 ? len2 : improve3 ? len3 : best;
-                bd = improve ? q - c : improve2 ? q - cn : improve3 ? q - cnn : bd;
+                const bool rej3 = T4 & test3 & !go3 & !improve3;
+                const unsigned cl3 = cl2 - test3;
+                const bool term4 = rej3 & ((cnnn == NONE) | (q - cnnn > max_dist) | (cl3 == 0));
+                const bool test4 = rej3 & !term4;
+                const bool quick4 = test4 & (best < maxl) & (cb4 == qb) & (k4 > 0);
+                const bool go4 = quick4 & (k4 == 8) & (maxl > 8);
+                const unsigned len4 = k4 < maxl ? k4 : maxl;
+                const bool improve4 = quick4 & !go4 & (len4 > best);
+                best = improve ? len : improve2 ? len2 : improve3 ? len3 : improve4 ? len4 : best;
+                bd = improve ? q - c : improve2 ? q - cn : improve3 ? q - cnn : improve4 ? q - cnnn : bd;
                 const bool found = term | (improve & (len >= nice)) | term2 | (improve2 & (len2 >= nice)) | term3 |
-                                   (improve3 & (len3 >= nice));
-                steps += test + test2 + test3;
-                chain_left = cl2 - test3;
-                const bool adv3 = rej2 & !found & !go3;               // c, cn, cnn done
+                                   (improve3 & (len3 >= nice)) | term4 | (improve4 & (len4 >= nice));
+                steps += test + test2 + test3 + test4;
+                chain_left = cl3 - test4;
+                const bool adv4 = rej3 & !found & !go4;               // c .. cnnn done
+                const bool adv3 = rej2 & !rej3 & !found & !go3;       // c, cn, cnn done
                 const bool adv2 = rej1 & !rej2 & !found & !go2;       // c and cn done
                 const bool adv1 = !rej1 & !found & ((test & !go_match) | (mt & !ext));
-                l = go_match || go2 || go3 ? 8u : ext ? l + 8 : 0u;
-                const unsigned c_new = adv3 ? cnnn : (adv2 || go3) ? cnn : (adv1 || go2) ? cn : c;
-                cn = adv3 ? c4 : (adv2 || go3) ? cnnn : (adv1 || go2) ? cnn : cn;
+                l = go_match || go2 || go3 || go4 ? 8u : ext ? l + 8 : 0u;
+                const unsigned c_new = adv4 ? c4 : (adv3 || go4) ? cnnn : (adv2 || go3) ? cnn : (adv1 || go2) ? cn : c;
+                cn = adv4 ? c5 : (adv3 || go4) ? c4 : (adv2 || go3) ? cnnn : (adv1 || go2) ? cnn : cn;
                 c = c_new;
-                mt = go_match || ext || go2 || go3;
+                mt = go_match || ext || go2 || go3 || go4;
 #else
                 // every load issued up front
                 const unsigned cc = c < wn ? c : 0;
