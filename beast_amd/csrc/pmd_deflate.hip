@@ -51,7 +51,10 @@ namespace dfl {
 constexpr unsigned CHUNK = 4096;
 constexpr unsigned HB = 11;
 constexpr unsigned HSIZE = 1u << HB;
-constexpr unsigned MIN_SEG = 32;
+#ifndef BPMD_MIN_SEG
+#define BPMD_MIN_SEG 16
+#endif
+constexpr unsigned MIN_SEG = BPMD_MIN_SEG;   // parse segment floor (bytes per lane)
 // A lane whose finds have walked more than BPMD_CHAIN_BUDGET chain candidates
 // per 64 bytes of its parse segment walks at most 4 per find from then on
 // (0 = no budget): the busiest lane sets a chunk's parse time

@@ -19,7 +19,7 @@ LIB = os.path.join(HERE, "_build", "libdmodel.so")
 _L = None
 
 # kernel constants (beast_amd/csrc/pmd_deflate.hip)
-CHUNK, HBITS, LANES, MIN_SEG = 4096, 11, 64, 32
+CHUNK, HBITS, LANES, MIN_SEG = 4096, 11, 64, 16
 
 
 def build():
