@@ -54,7 +54,7 @@ constexpr unsigned HSIZE = 1u << HB;
 #ifndef BPMD_MIN_SEG
 #define BPMD_MIN_SEG 16
 #endif
-constexpr unsigned MIN_SEG = BPMD_MIN_SEG;   // parse segment floor (bytes per lane)
+constexpr unsigned MIN_SEG = BPMD_MIN_SEG;   // parse segment floor (bytes per lane) of a chunk without history
 // A lane whose finds have walked more than BPMD_CHAIN_BUDGET chain candidates
 // per 64 bytes of its parse segment walks at most 4 per find from then on
 // (0 = no budget): the busiest lane sets a chunk's parse time
@@ -922,7 +922,11 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
         [[maybe_unused]] unsigned steps = 0, finds = 0, iters = 0;
         // ---- parse (head table dead from here; tok[] reuses it)
         unsigned seg = (clen + WAVE - 1) / WAVE;
-        seg = seg < MIN_SEG ? MIN_SEG : seg;
+        // (a chunk with history keeps 32: its matches reach back across more
+        // segment boundaries -- C1's takeover messages 1.0438 -> 1.0516x
+        // Beast's size at 16)
+        const unsigned min_seg = a0 ? 32u : MIN_SEG;
+        seg = seg < min_seg ? min_seg : seg;
         const unsigned a = a0 + lane * seg;
         const unsigned b = a + seg < wn ? a + seg : wn;
         const bool active = a < wn;

@@ -180,7 +180,8 @@ static std::vector<uint8_t> encode(const uint8_t* msg, unsigned n, const Params&
             }
             unsigned len = wn - a0;
             unsigned seg = (len + P.lanes - 1) / P.lanes;
-            if (seg < (unsigned)P.min_seg) seg = P.min_seg;
+            const unsigned min_seg = a0 ? 32u : (unsigned)P.min_seg;   // (pmd_deflate.hip: history keeps 32)
+            if (seg < min_seg) seg = min_seg;
             unsigned E = a0;
             for (unsigned s = a0; s < wn; s += seg) {
                 unsigned b = s + seg < wn ? s + seg : wn;
