@@ -70,6 +70,19 @@ LZ_HD Level level_params(int level)
 #ifndef BPMD_CHUNK_HIST
 #define BPMD_CHUNK_HIST 2048
 #endif
+// Levels >= BPMD_DEEP_LEVEL (zlib's slow levels 7-9) give each chunk 4 KiB of
+// history instead (round 5; C4 at 4 KiB and chain cap 32: 1.038x Beast's size
+// at 20.6 GiB/s against 1.059x at 30.5 with 2 KiB): the chunk
+// kernel's LDS then holds 5 waves per CU instead of 6.
+#ifndef BPMD_DEEP_LEVEL
+#define BPMD_DEEP_LEVEL 7
+#endif
+constexpr unsigned CHUNK_HIST_DEEP = 4096;
+LZ_HD unsigned chunk_hist(int level)
+{
+    return level >= BPMD_DEEP_LEVEL && CHUNK_HIST_DEEP > (unsigned)BPMD_CHUNK_HIST ? CHUNK_HIST_DEEP
+                                                                                   : (unsigned)BPMD_CHUNK_HIST;
+}
 LZ_HD unsigned gpu_chain(int level, bool single_chunk)
 {
     const unsigned c = level_params(level).chain;

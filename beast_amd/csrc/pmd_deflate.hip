@@ -36,6 +36,7 @@
 //   7. bit packing: per-lane bit counts, wave prefix sum, ds_or into an LDS
 //      bit buffer, dword stores to the output slot.
 #include <atomic>
+#include <type_traits>
 
 #include <mutex>
 
@@ -1966,19 +1967,29 @@ int deflate_impl(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_l
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     P.chain = chain(false);
-    if (total) {
-        const unsigned per_cu = (160u * 1024u) / (unsigned)sizeof(DefLds<CHUNK_HIST>);
+    // the chunk kernel with the level's history (lz::chunk_hist: 2 KiB, or 4 KiB
+    // at the slow levels)
+    auto launch_chunks = [&](auto hist_tag) -> int {
+        constexpr int H = decltype(hist_tag)::value;
+        const unsigned per_cu = (160u * 1024u) / (unsigned)sizeof(DefLds<H>);
         const unsigned grid = total < (uint32_t)cus * per_cu ? total : (unsigned)cus * per_cu;
         if (stitch) {
-            hipLaunchKernelGGL(deflate_chunks_kernel<CHUNK_HIST>, dim3(grid), dim3(64), 0, stream, in, in_off, in_len,
-                               items, first, d_total, slots, bits, d_total + 32, P);
+            hipLaunchKernelGGL(deflate_chunks_kernel<H>, dim3(grid), dim3(64), 0, stream, in, in_off, in_len, items,
+                               first, d_total, slots, bits, d_total + 32, P);
         } else {
             unsigned long long* ends = (unsigned long long*)(ws + o_bits);
-            if ((he = hipMemsetAsync(ends, 0, 8ull * total, stream)) != hipSuccess) return (int)he;
-            hipLaunchKernelGGL(deflate_chunks1_kernel<CHUNK_HIST>, dim3(grid), dim3(64), 0, stream, in, in_off, in_len,
-                               items, first, d_total, ends, out, out_off, out_cap, out_len, status, all,
-                               d_total + 32, P);
+            hipError_t e2 = hipMemsetAsync(ends, 0, 8ull * total, stream);
+            if (e2 != hipSuccess) return (int)e2;
+            hipLaunchKernelGGL(deflate_chunks1_kernel<H>, dim3(grid), dim3(64), 0, stream, in, in_off, in_len, items,
+                               first, d_total, ends, out, out_off, out_cap, out_len, status, all, d_total + 32, P);
         }
+        return 0;
+    };
+    if (total) {
+        const int e = lz::chunk_hist(level) == lz::CHUNK_HIST_DEEP
+                          ? launch_chunks(std::integral_constant<int, (int)lz::CHUNK_HIST_DEEP>{})
+                          : launch_chunks(std::integral_constant<int, CHUNK_HIST>{});
+        if (e) return e;
     }
     // the stitch: every chunked message (BPMD_DEFLATE_STITCH=1, round 4), or
     // only the empty messages of a takeover batch (no chunk to finish them)

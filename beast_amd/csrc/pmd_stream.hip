@@ -168,10 +168,11 @@ int run_one(bpmd_stream* s, const uint8_t* in, size_t n, size_t out_cap, std::ve
     return BPMD_R_OK;
 }
 
-// the flushed bytes become history; only the last BPMD_CHUNK_HIST are used
+// the flushed bytes become history; only the last lz::chunk_hist(level) are
+// used (kept: the most any level uses)
 void add_history(bpmd_stream* s, const uint8_t* p, size_t n)
 {
-    constexpr size_t keep = BPMD_CHUNK_HIST;
+    constexpr size_t keep = lz::CHUNK_HIST_DEEP > BPMD_CHUNK_HIST ? lz::CHUNK_HIST_DEEP : BPMD_CHUNK_HIST;
     if (n >= keep) {
         s->hist.assign(p + n - keep, p + n);
         return;

@@ -330,4 +330,4 @@ extern "C" int dmodel_rle_check(const uint8_t* lens, int n, uint32_t* serial, ui
 }
 
 // history bytes before each chunk of a long message (the kernel's value)
-extern "C" int dmodel_chunk_hist() { return BPMD_CHUNK_HIST; }
+extern "C" int dmodel_chunk_hist(int level) { return (int)chunk_hist(level); }

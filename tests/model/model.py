@@ -54,7 +54,7 @@ def encode(data, off, lens, level=6, wbits=15, strategy=0):
     out = np.zeros(cap, np.uint8)
     oo = np.zeros(n, np.uint64)
     ol = np.zeros(n, np.uint32)
-    hist = lib().dmodel_chunk_hist()   # BPMD_CHUNK_HIST (lz_core.h)
+    hist = lib().dmodel_chunk_hist(level)   # lz::chunk_hist (lz_core.h): 2 KiB, 4 KiB at levels >= 7
     r = lib().dmodel_batch(data.ctypes.data, off.ctypes.data, lens.ctypes.data, n, level, wbits, strategy, CHUNK,
                            hist, HBITS, LANES, MIN_SEG, 0, out.ctypes.data, cap, oo.ctypes.data, ol.ctypes.data)
     assert r >= 0
