@@ -65,6 +65,8 @@ struct alignas(16) Lds {
     WaveTableScratch ts;
     uint32_t ptok[ZQ * WAVE];   // pfast: a window's accepted tokens, (olen << 16) | literal or distance
     uint32_t pbm[ZBM];          // pfast: their first output byte, one bit per output byte of the window
+    uint32_t prec[ZQ * WAVE];   // pfast: the chain's tokens: candidate word A (bit fields, kind)
+    uint16_t poend[ZQ * WAVE];  // pfast: the bit after each, from the window's first bit
 };
 
 // cross-lane steps of pfast (one-lane meanings in the host build)
@@ -73,12 +75,31 @@ __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t j) { return (uin
 __device__ __forceinline__ uint64_t ballot64(bool p) { return __ballot(p); }
 __device__ __forceinline__ uint32_t shfl32(uint32_t v, uint32_t from) { return (uint32_t)__shfl((int)v, (int)from); }
 __device__ __forceinline__ uint32_t fsh(uint32_t hi, uint32_t lo, uint32_t sh) { return __builtin_amdgcn_alignbit(hi, lo, sh); }
+__device__ __forceinline__ uint32_t shfl_up32(uint32_t v, uint32_t d) { return (uint32_t)__shfl_up((int)v, d); }
+__device__ __forceinline__ uint32_t below64(uint64_t m)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 #else
 inline uint32_t rdlane(uint32_t v, uint32_t) { return v; }
 inline uint64_t ballot64(bool p) { return p ? 1u : 0u; }
 inline uint32_t shfl32(uint32_t v, uint32_t) { return v; }
 inline uint32_t fsh(uint32_t hi, uint32_t lo, uint32_t sh) { return (uint32_t)((((uint64_t)hi << 32) | lo) >> (sh & 31)); }
 inline void atomicOr(uint32_t* p, uint32_t v) { *p |= v; }
+inline uint32_t shfl_up32(uint32_t v, uint32_t) { return v; }
+inline uint32_t below64(uint64_t) { return 0; }
+#endif
+// pfast's byte-lag maps: fast()'s reservoir holds bn = r + 8 L bits at a token
+// boundary, r fixed by the bit position, L in 0..3 the refill history; a
+// token maps L before it to L after it (2 bits per entry, 4 entries)
+__host__ __device__ constexpr uint32_t lag_compose(uint32_t first, uint32_t then)
+{
+    uint32_t r = 0;
+    for (uint32_t x = 0; x < 4; ++x) r |= ((then >> (2 * ((first >> (2 * x)) & 3u))) & 3u) << (2 * x);
+    return r;
+}
+#ifndef BPMD_ZST_SCAN
+#define BPMD_ZST_SCAN 1   // 0: the scalar replay of round 5's first pfast
 #endif
 // a candidate token: A = c1 | x << 4 | c2 << 7 | dx << 11 | kind << 15 (bits of
 // the literal/length code incl. a sub-table's, length extra, distance code,
@@ -463,7 +484,8 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
             ZP_ADD(15, ZP_NOW() - zq);
             zq = ZP_NOW();
             // candidates at bits rb + lane + WAVE q of the staged input
-            uint32_t ca[ZQ], cb[ZQ];
+            const int64_t Ps = (int64_t)(ip * 8) - (int64_t)bn;   // the window's first bit (< 0: reservoir bits)
+            uint32_t ca[ZQ], cb[ZQ], cj[ZQ];
 #pragma unroll
             for (uint32_t q = 0; q < ZQ; ++q) {
                 const uint32_t r = rb + lane + WAVE * q, w = r >> 5, sh = r & 31;
@@ -498,23 +520,155 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
                         b = (len << 16) | dist;
                     }
                 }
+                // the bits this candidate consumes before fast() stops or goes on
+                const uint32_t k_ = a >> 15;
+                const uint32_t nb_ = k_ == Z_MATCH ? (a & 15u) + ((a >> 4) & 7u) + ((a >> 7) & 15u) + ((a >> 11) & 15u)
+                                                   : (a & 15u);
                 ca[q] = a;
                 cb[q] = b;
+                cj[q] = k_ == Z_LIT || k_ == Z_MATCH ? nb_ : 255u;   // the chain ends at an event
             }
             for (uint32_t i = lane; i < ZBM; i += WAVE) L.pbm[i] = 0;
             wave_sync();
             ZP_ADD(16, ZP_NOW() - zq);
             zq = ZP_NOW();
-            // the chain, replaying fast() (inflate_stream.ipp:979-1113)
             const uint64_t op0 = op;
-            uint32_t o = 0, acc = 0, wout = 0;
+            uint32_t acc = 0, wout = 0;
             bool needwin = false;
+#if BPMD_ZST_SCAN
+            // the chain of real token starts: one step per token on the scalar unit
+            uint64_t mm[ZQ];
+            {
+                uint32_t o = 0;
+#pragma unroll
+                for (uint32_t q = 0; q < ZQ; ++q) {
+                    uint64_t m = 0;
+                    while (o < WAVE * (q + 1)) {
+                        const uint32_t j = o - WAVE * q;
+                        m |= 1ull << j;
+                        o += rdlane(cj[q], j);
+                    }
+                    mm[q] = m;
+                }
+            }
+            // its tokens in order
+            uint32_t K = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < ZQ; ++q) {
+                if ((mm[q] >> lane) & 1ull) {
+                    const uint32_t rk = K + below64(mm[q]), a = ca[q], k_ = (a >> 15) & 7u;
+                    const uint32_t nb_ = k_ == Z_MATCH   ? (a & 15u) + ((a >> 4) & 7u) + ((a >> 7) & 15u) + ((a >> 11) & 15u)
+                                         : k_ == Z_BADDIST ? (a & 15u) + ((a >> 4) & 7u) + ((a >> 7) & 15u)
+                                                           : (a & 15u);
+                    L.prec[rk] = a;
+                    L.ptok[rk] = cb[q];
+                    L.poend[rk] = (uint16_t)(lane + WAVE * q + nb_);
+                }
+                K += (uint32_t)__builtin_popcountll(mm[q]);
+            }
+            wave_sync();
+            // fast() on them, 64 at a time: byte lags by a scan of lag maps,
+            // output offsets by a prefix sum, fast()'s checks per token, and
+            // the first token where fast() stops (or the window's output cap)
+            uint32_t Lc = ((uint32_t)bn - ((uint32_t)(-Ps) & 7u)) >> 3;   // bn = r + 8 L at the window's start
+            uint32_t wrel = 0;
+            for (uint32_t g = 0; g < K; g += WAVE) {
+                const uint32_t t = g + lane;
+                const bool act = t < K;
+                const uint32_t a = act ? L.prec[t] : 0u, b = act ? L.ptok[t] : 0u, oe = act ? L.poend[t] : 0u;
+                const uint32_t kind = (a >> 15) & 7u;
+                // the token's lag map: fast()'s refills for each byte lag before it
+                const uint32_t c1_ = a & 15u, x_ = (a >> 4) & 7u, c2_ = (a >> 7) & 15u, dx_ = (a >> 11) & 15u;
+                const uint32_t nb_ = kind == Z_MATCH ? c1_ + x_ + c2_ + dx_ : kind == Z_BADDIST ? c1_ + x_ + c2_ : c1_;
+                const uint32_t r_out = (uint32_t)(-(Ps + (int64_t)oe)) & 7u, r_in = (r_out + nb_) & 7u;
+                uint32_t f = 0;
+#pragma unroll
+                for (uint32_t lv = 0; lv < 4; ++lv) {
+                    uint32_t bq = r_in + 8 * lv;
+                    bq += bq < 15 ? 16u : 0u;
+                    bq -= c1_;
+                    if (kind == Z_MATCH || kind == Z_BADDIST) {
+                        if (bq < x_) bq += 8;
+                        bq -= x_;
+                        bq += bq < 15 ? 16u : 0u;
+                        bq -= c2_;
+                        if (kind == Z_MATCH) {
+                            if (bq < dx_) bq += 8;
+                            if (bq < dx_) bq += 8;
+                            bq -= dx_;
+                        }
+                    }
+                    f |= (((bq - r_out) >> 3) & 3u) << (2 * lv);
+                }
+                f = act ? f : 0xe4u;   // (identity map)
+#pragma unroll
+                for (uint32_t d = 1; d < WAVE; d <<= 1) {
+                    const uint32_t y = shfl_up32(f, d);
+                    f = lane >= d ? lag_compose(y, f) : f;
+                }
+                const uint32_t La = (f >> (2 * Lc)) & 3u;
+                uint32_t osum = act && (kind == Z_LIT || kind == Z_MATCH) ? b >> 16 : 0u;
+                const uint32_t olen = osum;
+#pragma unroll
+                for (uint32_t d = 1; d < WAVE; d <<= 1) {
+                    const uint32_t y = shfl_up32(osum, d);
+                    osum += lane >= d ? y : 0u;
+                }
+                const uint32_t oafter = wrel + osum, obefore = oafter - olen;
+                const uint64_t ipa = (uint64_t)(((Ps + (int64_t)oe + 7) >> 3) + (int64_t)La);
+                const uint64_t dist = b & 0xffffu, opb = op0 + obefore;
+                const bool ev = act && (kind == Z_EOB || kind == Z_BADLIT || kind == Z_BADDIST);
+                const bool bdist = act && kind == Z_MATCH && dist > opb && dist - opb > wsize;
+                const bool ok = act && !ev && !bdist;
+                const bool lstop = ok && !(ipa < in_last && op0 + oafter < out_last);
+                const bool wcap = ok && oafter >= ZWOUT;
+                const uint64_t sm = ballot64(ev || bdist || lstop || wcap);
+                const uint32_t first = sm ? (uint32_t)__builtin_ctzll(sm) : (uint32_t)WAVE;
+                const bool okf = first < WAVE && rdlane(ok ? 1u : 0u, first) != 0;
+                const bool take = act && (lane < first || (lane == first && okf));
+                if (take) atomicOr(&L.pbm[obefore >> 5], 1u << (obefore & 31));
+                needwin = needwin || ballot64(take && kind == Z_MATCH && dist > opb) != 0;
+                const uint32_t last = first < WAVE ? first : (K - g < WAVE ? K - g : (uint32_t)WAVE) - 1;
+                const int64_t Pe = Ps + (int64_t)rdlane(oe, last);
+                const uint32_t Le = rdlane(La, last);
+                acc = g + last + (first < WAVE && !okf ? 0u : 1u);
+                wrel = rdlane(first < WAVE && !okf ? obefore : oafter, last);
+                Lc = Le;
+                if (first < WAVE || g + WAVE >= K) {
+                    // fast()'s state after that token
+                    ip = (uint64_t)((Pe + 7) >> 3) + Le;
+                    bn = (uint32_t)((int64_t)(ip * 8) - Pe);
+                    if (first < WAVE) {
+                        const uint32_t kf = rdlane(kind, first);
+                        if (kf == Z_EOB) {
+                            h.mode = TYPE;
+                            stop = true;
+                        } else if (kf == Z_BADLIT) {
+                            err = ST_INVALID_LITERAL_LENGTH;
+                            stop = true;
+                        } else if (kf == Z_BADDIST) {
+                            err = ST_INVALID_DISTANCE_CODE;
+                            stop = true;
+                        } else if (rdlane(bdist ? 1u : 0u, first)) {
+                            err = ST_INVALID_DISTANCE;
+                            stop = true;
+                        } else if (rdlane(lstop ? 1u : 0u, first)) {
+                            stop = true;
+                        }   // else the window's output cap: the next window goes on
+                    }
+                    break;
+                }
+            }
+            wout = wrel;
+#else
+            // the chain, replaying fast() (inflate_stream.ipp:979-1113)
+            uint32_t o = 0;
 #pragma unroll
             for (uint32_t q = 0; q < ZQ; ++q) {
                 while (!stop && o < WAVE * (q + 1) && wout < ZWOUT) {
                     const uint32_t a = rdlane(ca[q], o - WAVE * q);
                     const uint32_t c1 = a & 15u, x = (a >> 4) & 7u, c2 = (a >> 7) & 15u, dx = (a >> 11) & 15u,
-                                   kind = a >> 15;
+                                   kind = (a >> 15) & 7u;
                     if (bn < 15) {   // pull(); pull();
                         ip += 2;
                         bn += 16;
@@ -578,6 +732,7 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
                     if (!(ip < in_last && op0 + wout < out_last)) stop = true;
                 }
             }
+#endif
             ZP_ADD(21, 1);
             ZP_ADD(22, acc);
             ZP_ADD(17, ZP_NOW() - zq);
