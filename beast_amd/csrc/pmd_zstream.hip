@@ -984,6 +984,7 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
             h.mode = LEN;
             [[fallthrough]];
         case LEN: {
+        len_again:   // (the next symbol without a trip through the switch)
             if (n_in - ip >= 6 && cap - op >= 258) {
                 const int32_t e = par && n_in - ip >= ZMIN_IN && cap - op >= ZMIN_OUT ? pfast() : fast();
                 if (e) {
@@ -1004,9 +1005,14 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
             }
             const uint32_t kind = slot_kind(s), val = slot_val(s);
             if (kind == K_VAL) {
-                h.length = val;
-                h.mode = LIT;
-                continue;
+                // LIT, in place: the byte, or LIT kept for the next call
+                if (op == cap) {
+                    h.length = val;
+                    h.mode = LIT;
+                    goto done;
+                }
+                put(val);
+                goto len_again;
             }
             if (kind == K_EOB) {
                 h.mode = TYPE;
@@ -1073,8 +1079,11 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
             if (n > cap - op) n = cap - op;
             copy_back(h.offset, (uint32_t)n);
             h.length -= (uint32_t)n;
-            if (h.length == 0) h.mode = LEN;
             if (op - flushed >= FLUSH_AT) flush_out();
+            if (h.length == 0) {
+                h.mode = LEN;
+                goto len_again;
+            }
             continue;
         }
         case LIT:
