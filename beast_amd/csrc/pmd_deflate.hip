@@ -1642,11 +1642,17 @@ deflate_chunks1_kernel(const uint8_t* __restrict__ in, const uint64_t* __restric
             uint32_t B = bit >> 3, Pb = 0, start = bit, end = bit, ecv = 0, hdr = 0;
             if (!ovf) {
                 if (o.stored) {
-                    // 000 at bit, pad, LEN NLEN at Pb, then the bytes
+                    // 000 at bit, pad, LEN NLEN at Pb, then the bytes; chunk 1
+                    // first gets the marker (hdr 3: 000, pad, 00 00 FF FF, then
+                    // the stored block's 000 and pad in one byte)
                     Pb = (bit + 3 + 7) >> 3;
+                    hdr = 1;
+                    if (c == 1) {
+                        Pb += 5;
+                        hdr = 3;
+                    }
                     if (Pb + 4 + L + 1 > cap) ovf = true;
                     end = (Pb + 4 + L) * 8;
-                    hdr = 1;
                 } else {
                     if (c > 0) {   // the empty stored block (sync marker) before the block
                         Pb = (bit + 3 + 7) >> 3;
@@ -1686,17 +1692,19 @@ deflate_chunks1_kernel(const uint8_t* __restrict__ in, const uint64_t* __restric
             if (hdr) {
                 // the byte holding the predecessor's last bits (and the 000 header
                 // bits), the pad byte if the header crosses it, LEN NLEN
+                const uint32_t Pm = hdr == 3 ? Pb - 5 : Pb;   // the first LEN field after the header bits
                 if (lane == 0) {
                     ob[B] = (uint8_t)cv ^ km(B);
-                    if (Pb - B == 2) ob[B + 1] = km(B + 1);
+                    if (Pm - B == 2) ob[B + 1] = km(B + 1);
                 }
-                const uint32_t lv = hdr == 1 ? L : 0u;
+                if (hdr == 3 && lane < 5) ob[Pm + lane] = (uint8_t)(lane < 2 ? 0x00 : lane < 4 ? 0xff : 0x00) ^ km(Pm + lane);
+                const uint32_t lv = hdr != 2 ? L : 0u;
                 if (lane < 4) {
                     const uint32_t w = lv | ((~lv & 0xffffu) << 16);
                     ob[Pb + lane] = (uint8_t)(w >> (8 * lane)) ^ km(Pb + lane);
                 }
             }
-            if (hdr == 1) {
+            if (hdr == 1 || hdr == 3) {
                 const uint8_t* src = msg + c * CHUNK;
                 for (uint32_t j = lane; j < L; j += WAVE) ob[Pb + 4 + j] = src[j] ^ km(Pb + 4 + j);
             } else {
@@ -1756,6 +1764,20 @@ stitch_kernel(const uint32_t* __restrict__ in_len, uint32_t n, uint32_t all, con
             if (w == 0xFFFFFFFFu) { overflow = true; break; }
             const uint8_t* t = temp + (size_t)k * SLOT;
             const uint32_t L = w & 0x7FFFFFFFu;
+            if (c == 1 && (w & 0x80000000u)) {
+                // a stored chunk 1 gets the marker too, so every payload of two
+                // or more chunks carries one and a block-parallel inflater
+                // knows its Huffman blocks are all marked (pmd_inflate_bp.hip)
+                const uint32_t B = bit >> 3, P = (bit + 3 + 7) >> 3;
+                if (P + 4 + 1 > cap) { overflow = true; break; }
+                if (lane == 0) {
+                    o[B] = (uint8_t)cv ^ km(B);
+                    if (P - B == 2) o[B + 1] = km(B + 1);
+                }
+                if (lane < 4) o[P + lane] = (uint8_t)(lane < 2 ? 0x00 : 0xff) ^ km(P + lane);
+                bit = (P + 4) * 8;
+                cv = 0;
+            }
             const uint32_t B = bit >> 3, s = bit & 7;
             if (w & 0x80000000u) {
                 // stored block: 000 at `bit`, pad to a byte, then LEN NLEN and the

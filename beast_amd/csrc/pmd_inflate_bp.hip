@@ -485,8 +485,31 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
         bool need = false;
         if (gl < n_regions && tasks[gl].kind == KIND_PENDING) {
             const uint32_t ri = region_map[gl];
-            if (marked[ri] || (gl - task_base[ri]) % dyn_stride != 0) tasks[gl].kind = KIND_NONE;
-            else need = true;
+            if (marked[ri] || (gl - task_base[ri]) % dyn_stride != 0) {
+                tasks[gl].kind = KIND_NONE;
+            } else {
+                // a region inside the data of a stored block pass 1 found (one
+                // of the 8 regions before it) holds no block start: no search
+                // (this library's incompressible chunks go stored without a
+                // marker; Beast's binary payloads are 35-60 % stored blocks)
+                const uint32_t k = gl - task_base[ri], R = stats[ri].R;
+                bool inside = false;
+                for (uint32_t j = 1; j <= 8 && j <= k; ++j) {
+                    const uint32_t kj = tasks[gl - j].kind;
+                    const uint8_t* pm = in + in_off[order[ri]];
+                    // (region 0 is the payload's start: a stored first block
+                    // has its LEN field at byte 1)
+                    if (kj == KIND_STORED || (j == k && ((pm[0] >> 1) & 3u) == 0)) {
+                        const uint32_t pb = kj == KIND_STORED ? tasks[gl - j].bit >> 3 : 1u;
+                        const uint32_t d0 = pb + 4, d1 = d0 + ((uint32_t)pm[pb] | (uint32_t)pm[pb + 1] << 8);
+                        inside = d0 <= k * R && (k + 1) * R <= d1;
+                        break;
+                    }
+                    if (kj != KIND_PENDING && kj != KIND_NONE) break;
+                }
+                if (inside) tasks[gl].kind = KIND_NONE;
+                else need = true;
+            }
         }
         todo = __ballot(need);
     }

@@ -146,8 +146,9 @@ static std::vector<uint8_t> encode(const uint8_t* msg, unsigned n, const Params&
     unsigned max_dist = wsize - LOOKAHEAD_MIN;
     std::vector<int32_t> prev;
     std::vector<int32_t> head(1u << P.hbits);
-    // the stitch's marker before every Huffman-coded chunk but the first: an
-    // empty stored block, so the block starts on a byte
+    // the stitch's marker before every Huffman-coded chunk but the first, and
+    // before chunk 1 whatever its kind: an empty stored block, so the block
+    // starts on a byte
     auto marker = [&](unsigned base) {
         if (!base) return;
         bw.put(0, 3);
@@ -253,6 +254,7 @@ static std::vector<uint8_t> encode(const uint8_t* msg, unsigned n, const Params&
         uint64_t opt_b = (dyn_bits + 7) >> 3, fix_b = (fix_bits + 7) >> 3;
         if (P.strategy == 4) opt_b = fix_b + 1;
         if (L.parser == P_STORED || (uint64_t)clen + 4 <= (opt_b < fix_b ? opt_b : fix_b)) {
+            if (base == (unsigned)P.chunk) marker(base);   // chunk 1 carries a marker whatever its kind
             bw.put(0, 3);
             bw.align();
             bw.put(clen & 0xFFFF, 16);
