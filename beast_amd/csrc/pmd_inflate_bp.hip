@@ -419,6 +419,13 @@ __device__ bool stored_ok(const GlobalBits& G, const LdsBits& Lb, uint32_t bias,
     return type == 1 && L == 0;
 }
 
+// the most compressed bytes from one of this library's markers (or a stored
+// block, or the payload's start) to the next: a 4 KiB chunk's block (stored
+// at worst: 4 096 + 5) plus the next marker
+constexpr uint32_t MARK_SPAN = 4096 + 5 + 5 + 16;
+#ifndef BPMD_BP_MARK_END
+#define BPMD_BP_MARK_END 1   // 0: any marker marks the payload (round 5 until the ADVICE fix)
+#endif
 constexpr uint32_t LIST = 128;         // candidate offsets per wave and chunk
 constexpr uint32_t CHUNK_STEPS = 4;    // 4 x 2048 bit offsets between deep-check rounds
 constexpr uint32_t STORED_FLAG = 0x80000000u;
@@ -485,7 +492,10 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
         bool need = false;
         if (gl < n_regions && tasks[gl].kind == KIND_PENDING) {
             const uint32_t ri = region_map[gl];
-            if (marked[ri] || (gl - task_base[ri]) % dyn_stride != 0) {
+            // (marked: bit 0 a sync marker, bit 1 a stored candidate within
+            // MARK_SPAN + R of the payload's end -- a foreign encoder's payload
+            // that flushed once near its start is searched)
+            if ((marked[ri] | (BPMD_BP_MARK_END ? 0u : 2u)) == 3u || (gl - task_base[ri]) % dyn_stride != 0) {
                 tasks[gl].kind = KIND_NONE;
             } else {
                 // a region inside the data of a stored block pass 1 found (one
@@ -610,13 +620,22 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
                             atomicAdd(&g_bp_diag[8], t1 - t0);
                             atomicAdd(&g_bp_diag[9], t2 - t1);
                         })
+                // near the end: this library's deflater starts a block at least
+                // every MARK_SPAN bytes, so its last regions hold a marker or a
+                // stored block (or the payload is that short).  Two spans: a
+                // last stored chunk is no candidate (Flush::sync's stripped
+                // header follows it, not a whole block)
+                const bool near_end = (k + 1) * st.R + st.R + 2 * MARK_SPAN >= len;
                 if (k == 0) {
-                    if (best != 0xffffffffu && best_len == 0 && lane == 0) atomicOr(&marked[i], 1u);
+                    if (lane == 0) {
+                        if (best != 0xffffffffu && best_len == 0) atomicOr(&marked[i], 1u);
+                        if (len <= 2 * MARK_SPAN || (best != 0xffffffffu && near_end)) atomicOr(&marked[i], 2u);
+                    }
                     kind = KIND_START;
                 } else if (best != 0xffffffffu) {
                     bit = best;
                     kind = KIND_STORED;
-                    if (best_len == 0 && lane == 0) atomicOr(&marked[i], 1u);
+                    if (lane == 0) atomicOr(&marked[i], (best_len == 0 ? 1u : 0u) | (near_end ? 2u : 0u));
                     BP_DIAG(if (lane == 0) atomicAdd(&g_bp_diag[5], 1ull));
                 } else if (!DYN) {
                     kind = KIND_PENDING;
@@ -755,7 +774,7 @@ bp_skim_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
     const SegTask t0 = tasks[g];
     if (t0.kind != KIND_START && t0.kind != KIND_STORED) continue;
     const uint32_t i = region_map[g];
-    if (marked[i]) continue;   // sync markers: pass 1 found the chunk starts
+    if (marked[i] == 3u) continue;   // sync markers: pass 1 found the chunk starts
     const Stat st = stats[i];
     const uint32_t tb = task_base[i];
     const uint32_t k0 = g - tb;

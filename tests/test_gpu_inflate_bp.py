@@ -218,6 +218,33 @@ def test_c5_payload_with_false_stored_candidate(level):
     assert c[0] == 1 and c[1] >= 8 and c[2] == 0, list(c)[:3]   # one payload, its segments, no fallback
 
 
+def test_foreign_payload_with_one_early_flush():
+    """A foreign encoder's payload whose only sync flush is near its start
+    (CPython's zlib, raw deflate, memLevel 4: Z_SYNC_FLUSH after the first
+    KiB, then ~1 KiB dynamic blocks without markers).  Pass 1 marks it (an
+    empty stored block), but pass 2 still searches every region farther than
+    MARK_SPAN from the last marker or stored block (pmd_inflate_bp.hip), so
+    the payload is cut at its dynamic headers instead of decoding as one
+    serial segment: exact output, many segments, no fallback."""
+    import ctypes
+    import zlib
+    pmd = _pmd()
+    msg = _data("json", 256 * 1024, 7)
+    co = zlib.compressobj(6, zlib.DEFLATED, -15, 4)
+    p = co.compress(msg[:1024]) + co.flush(zlib.Z_SYNC_FLUSH) + co.compress(msg[1024:]) + co.flush(zlib.Z_SYNC_FLUSH)
+    assert p.endswith(b"\x00\x00\xff\xff")
+    payloads = [p[:-4]] * 4
+    c = (ctypes.c_ulonglong * 12)()
+    pmd.lib().bpmd_diag_bp_counters(c, 1)
+    assert pmd.lib().bpmd_set_inflate_kernel(3) == 0
+    try:
+        _check(payloads, len(msg) + 16)
+    finally:
+        pmd.lib().bpmd_set_inflate_kernel(0)
+    pmd.lib().bpmd_diag_bp_counters(c, 1)
+    assert c[0] == 4 and c[1] >= 4 * 16 and c[2] == 0, list(c)[:4]
+
+
 # ---------------------------------------------------- workspace sizing (r05)
 # A stream's block-parallel decode workspace is sized on its first call (one
 # read-back) or by bpmd_inflate_reserve; payloads over the capacity are
