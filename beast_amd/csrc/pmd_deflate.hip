@@ -1516,6 +1516,18 @@ __global__ void __launch_bounds__(256) fill_items_kernel(const uint32_t* __restr
     }
 }
 
+// One message whose chunk count the host knows (a stream's write): the work
+// of the count, the scan and fill_items_kernel in one launch -- the counters
+// zeroed, first = {0, total}, every item message 0
+__global__ void __launch_bounds__(64) one_msg_setup_kernel(uint32_t* __restrict__ d_total, uint32_t* __restrict__ first,
+                                                           uint32_t* __restrict__ items, uint32_t total)
+{
+    const uint32_t t = threadIdx.x;
+    d_total[t] = t == 0 ? total : 0u;   // (the 256 bytes the memset clears otherwise)
+    if (t < 2) first[t] = t ? total : 0u;
+    for (uint32_t c = t; c < total; c += 64) items[c] = 0;
+}
+
 template <int HIST>
 __global__ void __launch_bounds__(64)
 deflate_chunks_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
@@ -1917,10 +1929,16 @@ int deflate_impl(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_l
     // and runs meanwhile)
     uint32_t* d_total = (uint32_t*)bpmd_internal_scratch(stream, 256, 1);   // [0] chunk count, [32] chunk queue
     if (!d_total) return (int)hipErrorOutOfMemory;
-    hipError_t he = hipMemsetAsync(d_total, 0, 256, stream);
-    if (he != hipSuccess) return (int)he;
-    hipLaunchKernelGGL(count_chunks_kernel, dim3(n < 256 * 256 ? (n + 255) / 256 : 256), dim3(256), 0, stream, in_len, n,
-                       all, d_total);
+    // one message with its chunk count known (a stream's write): one setup
+    // launch below instead of the memset, the count, the scan and the fill
+    const bool one = n == 1 && host_chunks >= 0;
+    hipError_t he = hipSuccess;
+    if (!one) {
+        he = hipMemsetAsync(d_total, 0, 256, stream);
+        if (he != hipSuccess) return (int)he;
+        hipLaunchKernelGGL(count_chunks_kernel, dim3(n < 256 * 256 ? (n + 255) / 256 : 256), dim3(256), 0, stream, in_len,
+                           n, all, d_total);
+    }
     uint32_t total = 0;
     P.chain = chain(true);
     if (host_chunks >= 0) {
@@ -1968,8 +1986,9 @@ int deflate_impl(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_l
     hipcub::CountingInputIterator<uint32_t> idx(0);
     hipcub::TransformInputIterator<uint32_t, ChunkCountOp, hipcub::CountingInputIterator<uint32_t>> counts(
         idx, ChunkCountOp{in_len, n, all != 0});
-    if ((he = hipcub::DeviceScan::ExclusiveSum(nullptr, cub_bytes, counts, (uint32_t*)nullptr, n + 1, stream)) !=
-        hipSuccess)
+    if (!one &&
+        (he = hipcub::DeviceScan::ExclusiveSum(nullptr, cub_bytes, counts, (uint32_t*)nullptr, n + 1, stream)) !=
+            hipSuccess)
         return (int)he;
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t o_first = 0, o_items = up(o_first + 4ull * (n + 1)),
@@ -1982,10 +2001,14 @@ int deflate_impl(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_l
     uint32_t* items = (uint32_t*)(ws + o_items);
     uint32_t* bits = (uint32_t*)(ws + o_bits);
     uint8_t* slots = ws + o_slots;
-    if ((he = hipcub::DeviceScan::ExclusiveSum(ws + o_cub, cub_bytes, counts, first, n + 1, stream)) != hipSuccess)
-        return (int)he;
-    const unsigned fgrid = n < 256 * 1024 ? (n + 255) / 256 : 1024;
-    hipLaunchKernelGGL(fill_items_kernel, dim3(fgrid), dim3(256), 0, stream, in_len, n, all, first, items);
+    if (one) {
+        hipLaunchKernelGGL(one_msg_setup_kernel, dim3(1), dim3(64), 0, stream, d_total, first, items, total);
+    } else {
+        if ((he = hipcub::DeviceScan::ExclusiveSum(ws + o_cub, cub_bytes, counts, first, n + 1, stream)) != hipSuccess)
+            return (int)he;
+        const unsigned fgrid = n < 256 * 1024 ? (n + 255) / 256 : 1024;
+        hipLaunchKernelGGL(fill_items_kernel, dim3(fgrid), dim3(256), 0, stream, in_len, n, all, first, items);
+    }
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     P.chain = chain(false);
