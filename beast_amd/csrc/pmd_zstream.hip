@@ -147,19 +147,29 @@ enum : int { F_BLOCK = 1, F_FINISH = 5, F_TREES = 6 };   // zlib::Flush values t
 // staging; counts: 9 copies, 10 fast-loop tokens, 11 output bytes, 12
 // stagings, 13 calls, 14 input bytes; inside inflate_fast: 15 bit refill +
 // literal/length lookup, 16 literal store, 17 length extra + distance decode,
-// 18 loop tail, 19 the cost of one lap (two clock reads)
+// 18 loop tail, 19 the cost of one lap (two clock reads); 24 symbols decoded
+// by the slow path (LEN mode), 25 slow-path cycles (LEN .. MATCH), 26 block
+// headers (TYPEDO)
+constexpr int ZPN = 32;
 #ifndef BPMD_ZSTREAM_HOST
-__device__ unsigned long long g_zprof[24];
+__device__ unsigned long long g_zprof[ZPN];
 #endif
 #if defined(BPMD_PROF) && !defined(BPMD_ZSTREAM_HOST)
 #define ZP_NOW() ((unsigned long long)__builtin_amdgcn_s_memtime())
 #define ZP_ADD(i, v) (zp[i] += (unsigned long long)(v))
-#define ZP_DECL unsigned long long zp[24] = {};
+#define ZP_DECL unsigned long long zp[ZPN] = {};
 #define ZP_FLUSH() \
     do { \
         if (lane == 0) \
-            for (int i_ = 0; i_ < 24; ++i_) atomicAdd(&g_zprof[i_], zp[i_]); \
+            for (int i_ = 0; i_ < ZPN; ++i_) atomicAdd(&g_zprof[i_], zp[i_]); \
     } while (0)
+#elif defined(BPMD_ZSTREAM_HOST) && defined(BPMD_ZS_HOST_COUNT)
+// host model, counts only (tests/model/zstream_host.py, ZS_HOST_FLAGS)
+extern "C" { unsigned long long zs_host_counts[ZPN]; }
+#define ZP_NOW() 0ull
+#define ZP_ADD(i, v) (zs_host_counts[i] += (unsigned long long)(v))
+#define ZP_DECL
+#define ZP_FLUSH() ((void)0)
 #else
 #define ZP_NOW() 0ull
 #define ZP_ADD(i, v) ((void)0)
@@ -813,6 +823,7 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
                 h.mode = CHECK;
                 continue;
             }
+            ZP_ADD(26, 1);
             if (!fill(3)) goto done;
             h.last = take(1);
             const uint32_t t = take(2);
@@ -993,6 +1004,7 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
                 }
                 continue;
             }
+            ZP_ADD(24, 1);
             if (!fill(h.lroot)) goto done;
             uint32_t s = uni(L.tab[peek(h.lroot)]);
             if (is_link(s)) {
@@ -1189,10 +1201,10 @@ extern "C" int bpmd_internal_zstream_write(void* st, const uint8_t* in, uint64_t
 // diagnostic counters (meaningful only in the -DBPMD_PROF build)
 extern "C" int bpmd_diag_zstream_counters(unsigned long long* out, int reset)
 {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(bpmd::zst::g_zprof), sizeof(unsigned long long) * 24) != hipSuccess)
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(bpmd::zst::g_zprof), sizeof(unsigned long long) * bpmd::zst::ZPN) != hipSuccess)
         return -1;
     if (reset) {
-        unsigned long long z[24] = {0};
+        unsigned long long z[bpmd::zst::ZPN] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(bpmd::zst::g_zprof), z, sizeof z) != hipSuccess) return -1;
     }
     return 0;

@@ -28,8 +28,8 @@ def main():
     data, off, ln = synth.make_batch("json", [size] * n, seed=0x5EED0001)
     msgs = [bytes(data[int(off[i]):int(off[i]) + size]) for i in range(n)]
     L.bpmd_diag_deflate_counters.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    c = (ctypes.c_ulonglong * 24)()
-    dc = (ctypes.c_ulonglong * 24)()
+    c = (ctypes.c_ulonglong * 32)()
+    dc = (ctypes.c_ulonglong * 32)()
     for i, m in enumerate(msgs):
         if i == 8:
             L.bpmd_diag_zstream_counters(c, 1)
