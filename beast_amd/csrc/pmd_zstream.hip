@@ -160,7 +160,7 @@ __device__ unsigned long long g_zprof[ZPN];
 #define ZP_DECL unsigned long long zp[ZPN] = {};
 #define ZP_FLUSH() \
     do { \
-        if (lane == 0) \
+        if (lane == 0 && !(par & 4)) \
             for (int i_ = 0; i_ < ZPN; ++i_) atomicAdd(&g_zprof[i_], zp[i_]); \
     } while (0)
 #elif defined(BPMD_ZSTREAM_HOST) && defined(BPMD_ZS_HOST_COUNT)
@@ -809,7 +809,19 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
     int32_t data_type = 0;
 
     if (h.mode == TYPE) h.mode = TYPEDO;
+    // prof build: cycles between trips through the switch, by the mode the
+    // trip began in (27 type, 28 stored, 29 dynamic header, 30 LEN .. LIT)
+    [[maybe_unused]] unsigned long long zsw = ZP_NOW();
+    [[maybe_unused]] uint32_t zsm = h.mode;
+    auto zbucket = [](uint32_t m) { return m <= TYPEDO ? 27 : m <= COPY ? 28 : m <= CODELENS ? 29 : m <= LIT ? 30 : 31; };
+    (void)zbucket;
     for (;;) {
+        {
+            const unsigned long long n_ = ZP_NOW();
+            ZP_ADD(zbucket(zsm), n_ - zsw);
+            zsw = n_;
+            zsm = h.mode;
+        }
         switch (h.mode) {
         case HEAD:
             h.mode = TYPEDO;
@@ -997,7 +1009,7 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
         case LEN: {
         len_again:   // (the next symbol without a trip through the switch)
             if (n_in - ip >= 6 && cap - op >= 258) {
-                const int32_t e = par && n_in - ip >= ZMIN_IN && cap - op >= ZMIN_OUT ? pfast() : fast();
+                const int32_t e = (par & 1) && n_in - ip >= ZMIN_IN && cap - op >= ZMIN_OUT ? pfast() : fast();
                 if (e) {
                     ec = e;
                     goto quiet;
@@ -1119,6 +1131,7 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
 
 done:   // the done() lambda, inflate_stream.ipp:88-119
     ztd = ZP_NOW();
+    ZP_ADD(zbucket(zsm), ztd - zsw);
     flush_out();
     if (op && h.mode < BAD && (h.mode < CHECK || flush != F_FINISH)) {
         // window::write (window.hpp:109-141): the last min(n, capacity) bytes
@@ -1158,12 +1171,30 @@ quiet:
 }
 
 #ifndef BPMD_ZSTREAM_HOST
+#ifdef BPMD_PROF
+__device__ State g_warm_st;
+__device__ uint8_t g_warm_out[1 << 16];
+__device__ Result g_warm_res;
+#endif
 __global__ void __launch_bounds__(WAVE)
 zstream_write_kernel(State* __restrict__ st, const uint8_t* __restrict__ in, uint64_t n_in, uint8_t* __restrict__ out,
                      uint64_t cap, int flush, Result* __restrict__ res, int par)
 {
     __shared__ Lds L;
-    zstream_run(L, st, in, n_in, out, cap, flush, res, par);
+#ifdef BPMD_PROF
+    // diagnostics (BPMD_ZSTREAM_WARM=1): the same call first on a copy of the
+    // state, uncounted, so the counted call runs with warm caches
+    if (par & 2) {
+        static_assert(sizeof(State) % 4 == 0, "state copy in dwords");
+        for (unsigned i = lane_id(); i < sizeof(State) / 4; i += WAVE)
+            ((uint32_t*)&g_warm_st)[i] = ((const uint32_t*)st)[i];
+        __syncthreads();
+        zstream_run(L, &g_warm_st, in, n_in, g_warm_out, cap < sizeof g_warm_out ? cap : sizeof g_warm_out, flush,
+                    &g_warm_res, (par & 1) | 4);
+        __syncthreads();
+    }
+#endif
+    zstream_run(L, st, in, n_in, out, cap, flush, res, par & 1);
 }
 #endif
 
@@ -1192,7 +1223,14 @@ extern "C" int bpmd_internal_zstream_write(void* st, const uint8_t* in, uint64_t
         return e ? (atoi(e) ? 1 : 0) : 1;
     }();
     const int o = g_zst_par.load();
-    const int par = o < 0 ? env_par : o;
+    int par = o < 0 ? env_par : o;
+#ifdef BPMD_PROF
+    static const int env_warm = [] {
+        const char* e = getenv("BPMD_ZSTREAM_WARM");
+        return e && atoi(e) ? 2 : 0;
+    }();
+    par |= env_warm;
+#endif
     hipLaunchKernelGGL(zstream_write_kernel, dim3(1), dim3(bpmd::WAVE), 0, stream, (State*)st, in, n_in, out, cap,
                        flush, (Result*)res, par);
     return (int)hipGetLastError();

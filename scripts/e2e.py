@@ -6,6 +6,9 @@ of chunk i and the D2H of chunk i-1 overlap; nothing in the loop waits on
 the device).  Reported in DESIGN.md; never the bench `value`.
 
     python scripts/e2e.py [--chunks 8] [--reps 5]
+
+`*_copy_only_GiBps`: the same copies with no kernel (the PCIe bound of the
+pipeline).
 """
 import argparse
 import json
@@ -74,6 +77,30 @@ def run_pipeline(chunks, kernel, out_bytes_of, reps, depth=3):
     return sorted(times[1:])[len(times[1:]) // 2], outs_h, lens_h
 
 
+def copy_only(chunks, out_bytes_of, reps, depth=3):
+    """The same H2D and D2H byte counts, chunking and streams with no kernel:
+    what the PCIe link alone allows this pipeline (the e2e rate's bound)."""
+    dev = torch.device("cuda", 0)
+    streams = [torch.cuda.Stream() for _ in range(depth)]
+    maxin = max(c[0].numel() for c in chunks)
+    maxout = max(out_bytes_of(c[3]) for c in chunks)
+    slots = [dict(d=torch.empty(maxin + 64, dtype=torch.uint8, device=dev),
+                  out=torch.zeros(maxout + 64, dtype=torch.uint8, device=dev)) for _ in streams]
+    outs_h = [torch.empty(out_bytes_of(c[3]), dtype=torch.uint8).pin_memory() for c in chunks]
+    times = []
+    for _ in range(reps + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i, (hd, ho, hl, n) in enumerate(chunks):
+            sl = slots[i % depth]
+            with torch.cuda.stream(streams[i % depth]):
+                sl["d"][: hd.numel()].copy_(hd, non_blocking=True)
+                outs_h[i].copy_(sl["out"][: outs_h[i].numel()], non_blocking=True)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    return sorted(times[1:])[len(times[1:]) // 2]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--chunks", type=int, default=8)
@@ -100,6 +127,8 @@ def main():
     res["inflate_e2e_GiBps"] = round(n * mb / (1 << 30) / t, 3)
     res["inflate_e2e_ok"] = bool(np.array_equal(got, raw[: n * mb]))
     res["inflate_h2d_bytes"] = int(comp.nbytes)
+    tc = copy_only(chunks, lambda k: k * mb, a.reps, a.depth)
+    res["inflate_copy_only_GiBps"] = round(n * mb / (1 << 30) / tc, 3)
 
     # C3 deflate: messages in, payloads out (slots of upper_bound bytes)
     raw3, off3, len3 = synth.make_batch("json", lens, seed=bench.SEED_C3)
@@ -124,6 +153,8 @@ def main():
     res["deflate_e2e_spot_ok"] = bool(ok3)
     res["deflate_e2e_GiBps"] = round(n * mb / (1 << 30) / t3, 3)
     res["deflate_d2h_bytes"] = int(sum(int(x.numpy().sum()) for x in lens3))
+    tc3 = copy_only(chunks3, lambda k: k * slot, a.reps, a.depth)
+    res["deflate_copy_only_GiBps"] = round(n * mb / (1 << 30) / tc3, 3)
     res["chunks"] = a.chunks
     res["streams"] = a.depth
     print(json.dumps(res))
