@@ -67,6 +67,11 @@ constexpr unsigned MIN_SEG = BPMD_MIN_SEG;   // parse segment floor (bytes per l
 // next candidate of the chain, with the same limits and in the same order
 // (1), and in the chunk kernel (chain cap 32) a third after that (2; the
 // single-chunk kernel's walks are capped at 4 and lose with three)
+// BPMD_MIN_SEG_HIST: the parse segment floor of a chunk with history bytes
+// before it (the host model's min_seg with history)
+#ifndef BPMD_MIN_SEG_HIST
+#define BPMD_MIN_SEG_HIST 32
+#endif
 #ifndef BPMD_DUAL_TEST
 #define BPMD_DUAL_TEST 2
 #endif
@@ -926,7 +931,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
         // (a chunk with history keeps 32: its matches reach back across more
         // segment boundaries -- C1's takeover messages 1.0438 -> 1.0516x
         // Beast's size at 16)
-        const unsigned min_seg = a0 ? 32u : MIN_SEG;
+        const unsigned min_seg = a0 ? (unsigned)BPMD_MIN_SEG_HIST : MIN_SEG;
         seg = seg < min_seg ? min_seg : seg;
         const unsigned a = a0 + lane * seg;
         const unsigned b = a + seg < wn ? a + seg : wn;
