@@ -148,8 +148,8 @@ enum : int { F_BLOCK = 1, F_FINISH = 5, F_TREES = 6 };   // zlib::Flush values t
 // stagings, 13 calls, 14 input bytes; inside inflate_fast: 15 bit refill +
 // literal/length lookup, 16 literal store, 17 length extra + distance decode,
 // 18 loop tail, 19 the cost of one lap (two clock reads); 24 symbols decoded
-// by the slow path (LEN mode), 25 slow-path cycles (LEN .. MATCH), 26 block
-// headers (TYPEDO)
+// by the slow path (LEN mode), 25 code-length symbols hdr_par committed, 26
+// block headers (TYPEDO)
 constexpr int ZPN = 32;
 #ifndef BPMD_ZSTREAM_HOST
 __device__ unsigned long long g_zprof[ZPN];
@@ -181,6 +181,9 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
                             uint8_t* __restrict__ out, uint64_t cap, int flush, Result* __restrict__ res, int par)
 {
     const unsigned lane = lane_id();
+    // par: bit 0 the wave-parallel inflate_fast, bit 3 the serial code-length
+    // loop instead of hdr_par (diagnostics and tests; bits 1-2: prof build)
+    const bool hpar = !(par & 8);
     ZP_DECL
     const unsigned long long zt0 = ZP_NOW();
     unsigned long long zth = zt0, ztd = 0;
@@ -804,6 +807,119 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
         return err;
     };
 
+    // ---- the dynamic header's code lengths, wave-parallel (CODELENS).  Per
+    // window of ZQ * WAVE bit offsets from the next symbol's first bit, every
+    // lane decodes the code-length symbol (and its repeat bits) that would
+    // start at each of its offsets; the scalar unit follows the chain of real
+    // symbol starts; the lanes then write the lengths (repeat counts by a
+    // prefix sum, a 16's value from the last symbol before it that is not a
+    // 16).  The bytes the reference's fill() calls pull are a running maximum
+    // over the symbols (each pulls until it has max(root, code + repeat bits)),
+    // so ip / bn / bv after the window are the serial loop's.  Only symbols the
+    // serial loop would take without stopping are committed: one that lacks
+    // input, a 16 with no length before it, or a repeat past the end leaves the
+    // rest to the serial loop, which stops or fails exactly as the reference.
+    // Returns the symbols committed (0: nothing done).
+    auto hdr_par = [&](uint32_t want) -> uint32_t {
+        const uint32_t lroot = h.lroot, lmask = (1u << lroot) - 1u;
+        const uint32_t* iw = (const uint32_t*)L.ist;
+        const uint64_t S = ip * 8 - bn;   // the next symbol's first bit (bn <= ip * 8)
+        if ((S >> 3) < ib0 || (S >> 3) >= ib1 || (S >> 3) + ZSPAN > ib0 + IST) stage(S >> 3);
+        const uint32_t rb = (uint32_t)(S - 8 * ib0);
+        const uint32_t avail = (uint32_t)(8 * (ib1 - ib0));   // staged bits (ib1 <= n_in)
+        // candidate word: len | val << 4 | need << 9 | rep << 13 | ok << 21
+        uint32_t cw[ZQ];
+#pragma unroll
+        for (uint32_t q = 0; q < ZQ; ++q) {
+            const uint32_t r = rb + lane + WAVE * q, w = r >> 5, sh = r & 31;
+            const uint32_t d0 = iw[w], d1 = iw[w + 1];
+            const uint32_t v = fsh(d1, d0, sh);   // >= 32 valid bits; a symbol needs <= 14
+            const uint32_t sl = L.tab[v & lmask];
+            const uint32_t cb = slot_bits(sl);
+            const uint32_t val = slot_kind(sl) == K_SPECIAL ? 0u : slot_val(sl);
+            const uint32_t x = val == 16 ? 2u : val == 17 ? 3u : val == 18 ? 7u : 0u;
+            const uint32_t ev = (v >> cb) & ((1u << x) - 1u);
+            const uint32_t rep = val < 16 ? 1u : val == 18 ? 11u + ev : 3u + ev;
+            const uint32_t len = cb + x, need = len > lroot ? len : lroot;
+            const bool ok = r + need <= avail;
+            cw[q] = len | val << 4 | need << 9 | rep << 13 | (ok ? 1u : 0u) << 21;
+        }
+        // the chain, on the scalar unit
+        uint64_t mm[ZQ];
+        uint32_t have = h.have, o = 0, pulled = (uint32_t)(ip - ib0) * 8, n = 0;
+        bool stop = false;
+#pragma unroll
+        for (uint32_t q = 0; q < ZQ; ++q) {
+            uint64_t m = 0;
+            while (!stop && o < WAVE * (q + 1)) {
+                const uint32_t j = o - WAVE * q;
+                const uint32_t c = rdlane(cw[q], j);
+                const uint32_t val = (c >> 4) & 31u, rep = (c >> 13) & 255u;
+                if (!((c >> 21) & 1u) || (val == 16 && have == 0) || have + rep > want) {
+                    stop = true;
+                    break;
+                }
+                m |= 1ull << j;
+                have += rep;
+                ++n;
+                const uint32_t e = ((rb + o + ((c >> 9) & 15u) + 7u) & ~7u);   // bits pulled through this symbol
+                pulled = e > pulled ? e : pulled;
+                o += c & 15u;
+                if (have == want) stop = true;
+            }
+            mm[q] = m;
+        }
+        if (n == 0) return 0;
+        ZP_ADD(25, n);
+        // the lengths: rank of each chain symbol, its first slot and its value
+        uint32_t* rec = L.prec;   // rank -> val | rep << 8
+        wave_sync();
+        uint32_t K = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < ZQ; ++q) {
+            if ((mm[q] >> lane) & 1ull) rec[K + below64(mm[q])] = ((cw[q] >> 4) & 31u) | ((cw[q] >> 13) & 255u) << 8;
+            K += (uint32_t)__builtin_popcountll(mm[q]);
+        }
+        wave_sync();
+        uint32_t base = h.have;                                    // the first slot of this group
+        uint32_t prev = base ? uni(L.lens[base - 1]) : 0u;         // the length before it
+        for (uint32_t g = 0; g < n; g += WAVE) {
+            const uint32_t t = g + lane;
+            const uint32_t rv = t < n ? rec[t] : 0u, val = rv & 255u, rep = t < n ? rv >> 8 : 0u;
+            // inclusive prefix sums: repeat counts, and the last rank (+1) whose value is not a 16's
+            uint32_t sum = rep, last = t < n && val != 16 ? t + 1 : 0u;
+            for (uint32_t d = 1; d < WAVE; d <<= 1) {
+                const uint32_t s2 = shfl_up32(sum, d), l2 = shfl_up32(last, d);
+                if (lane >= d) {
+                    sum += s2;
+                    last = l2 > last ? l2 : last;
+                }
+            }
+            const uint32_t lastv = last ? rec[last - 1] & 255u : 0u;
+            const uint32_t src = last ? (lastv < 16 ? lastv : 0u) : prev;   // 17 / 18 write zeros
+            const uint32_t fv = val < 16 ? val : val == 16 ? src : 0u;
+            if (t < n)
+                for (uint32_t k = 0; k < rep; ++k) L.lens[base + sum - rep + k] = (uint8_t)fv;
+            const uint32_t gl = n - g < WAVE ? n - g - 1 : WAVE - 1;   // the group's last lane
+            const uint32_t tot = rdlane(sum, gl), fl = rdlane(fv, gl);
+            base += tot;
+            prev = fl;
+        }
+        wave_sync();
+        lens_dirty = true;
+        h.have = have;
+        // the reservoir after the last symbol: bytes pulled so far, bits past it
+        const uint32_t rend = rb + o;
+        ip = ib0 + (pulled >> 3);
+        bn = pulled - rend;
+        {
+            const uint32_t w = rend >> 5, sh = rend & 31;
+            const uint32_t v = fsh(uni(iw[w + 1]), uni(iw[w]), sh);
+            bv = bn >= 32 ? v : v & ((1u << bn) - 1u);
+        }
+        return n;
+    };
+
     int32_t ec = 0;
     int32_t published = 0;
     int32_t data_type = 0;
@@ -935,7 +1051,12 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
             [[fallthrough]];
         case CODELENS: {
             const uint32_t want = h.nlen + h.ndist;
+            bool hp = hpar;   // (off for the rest of the call once a window commits nothing)
             while (h.have < want) {
+                if (hp && want - h.have >= 8 && bn <= ip * 8) {
+                    if (hdr_par(want)) continue;
+                    hp = false;
+                }
                 if (!fill(h.lroot)) goto done;
                 const uint32_t s = uni(L.tab[peek(h.lroot)]);
                 const uint32_t cb = slot_bits(s);
@@ -1190,11 +1311,11 @@ zstream_write_kernel(State* __restrict__ st, const uint8_t* __restrict__ in, uin
             ((uint32_t*)&g_warm_st)[i] = ((const uint32_t*)st)[i];
         __syncthreads();
         zstream_run(L, &g_warm_st, in, n_in, g_warm_out, cap < sizeof g_warm_out ? cap : sizeof g_warm_out, flush,
-                    &g_warm_res, (par & 1) | 4);
+                    &g_warm_res, (par & 9) | 4);
         __syncthreads();
     }
 #endif
-    zstream_run(L, st, in, n_in, out, cap, flush, res, par & 1);
+    zstream_run(L, st, in, n_in, out, cap, flush, res, par & 9);
 }
 #endif
 
@@ -1208,9 +1329,11 @@ zstream_write_kernel(State* __restrict__ st, const uint8_t* __restrict__ in, uin
 // inflate_fast loop instead of the wave-parallel one (same results)
 static std::atomic<int> g_zst_par{-1};
 
+// on: -1 the environment's default, else bit 0 the wave-parallel
+// inflate_fast, bit 3 the serial code-length loop (BPMD_ZSTREAM_HPAR=0)
 extern "C" int bpmd_diag_set_zstream_parallel(int on)
 {
-    g_zst_par.store(on < 0 ? -1 : (on ? 1 : 0));
+    g_zst_par.store(on < 0 ? -1 : (on & 9));
     return 0;
 }
 
@@ -1220,7 +1343,8 @@ extern "C" int bpmd_internal_zstream_write(void* st, const uint8_t* in, uint64_t
     using namespace bpmd::zst;
     static const int env_par = [] {
         const char* e = getenv("BPMD_ZSTREAM_PAR");
-        return e ? (atoi(e) ? 1 : 0) : 1;
+        const char* hp = getenv("BPMD_ZSTREAM_HPAR");
+        return (e ? (atoi(e) ? 1 : 0) : 1) | (hp && hp[0] == '0' ? 8 : 0);
     }();
     const int o = g_zst_par.load();
     int par = o < 0 ? env_par : o;

@@ -40,7 +40,7 @@ def main():
     k = n - 8
     print(f"{k} messages of {size} B, {calls / k:.1f} calls per message; per message: "
           f"{cnt[10] / k:.1f} serial inflate_fast tokens, {cnt[22] / k:.1f} parallel ones in {cnt[21] / k:.1f} windows, "
-          f"{cnt[24] / k:.1f} slow-path symbol decodes, {cnt[26] / k:.1f} block headers, {cnt[9] / k:.1f} copies, "
+          f"{cnt[24] / k:.1f} slow-path symbol decodes, {cnt[25] / k:.1f} code-length symbols in parallel windows, {cnt[26] / k:.1f} block headers, {cnt[9] / k:.1f} copies, "
           f"{cnt[12] / k:.1f} stagings")
 
 

@@ -94,7 +94,8 @@ extern "C" int zs_host_write(void* st, const uint8_t* in, uint64_t n, uint8_t* o
     static thread_local bpmd::zst::Lds L;
     // BPMD_ZSTREAM_PAR=0: the serial inflate_fast loop (default: the parallel one, one lane)
     const char* e = getenv("BPMD_ZSTREAM_PAR");
-    const int par = e ? atoi(e) != 0 : 1;
+    const char* hp = getenv("BPMD_ZSTREAM_HPAR");   // 0: the serial code-length loop
+    const int par = (e ? atoi(e) != 0 : 1) | (hp && hp[0] == '0' ? 8 : 0);
     bpmd::zst::zstream_run(L, (bpmd::zst::State*)st, in, n, out, cap, flush, (bpmd::zst::Result*)res, par);
     return ((bpmd::zst::Result*)res)->ec;
 }

@@ -114,13 +114,15 @@ def test_errors_then_bad_mode():
     Z.case_errors(make)
 
 
-@pytest.mark.parametrize("par", [0, 1])
+@pytest.mark.parametrize("par", [0, 1, 8, 9])
 def test_serial_and_parallel_fast_loops(par):
     """inflate_fast runs wave-parallel by default (pmd_zstream.hip pfast: the
     lanes decode every candidate bit offset of a window, the scalar unit
-    replays inflate_fast on the chain of real token starts); the serial loop
-    it replays stays selectable (bpmd_diag_set_zstream_parallel /
-    BPMD_ZSTREAM_PAR=0).  Both must give the oracle's write()s."""
+    replays inflate_fast on the chain of real token starts), and so do the
+    dynamic header's code lengths (hdr_par); the serial loops they replay
+    stay selectable (bpmd_diag_set_zstream_parallel bit 0 = pfast, bit 3 =
+    the serial code-length loop; BPMD_ZSTREAM_PAR=0 / BPMD_ZSTREAM_HPAR=0).
+    Every combination must give the oracle's write()s."""
     L = _lib()
     L.bpmd_diag_set_zstream_parallel.argtypes = [ctypes.c_int]
     L.bpmd_diag_set_zstream_parallel(par)
@@ -130,6 +132,8 @@ def test_serial_and_parallel_fast_loops(par):
         Z.case_foreign_payloads(make)
         Z.case_errors(make)
         Z.case_small_window(make)
+        Z.case_byte_at_a_time_input(make)
+        Z.case_kat_split(make, every_cut=False)
     finally:
         L.bpmd_diag_set_zstream_parallel(-1)
 

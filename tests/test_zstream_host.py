@@ -23,6 +23,18 @@ def test_foreign_encoder_connection():
     Z.case_foreign_payloads(make)
 
 
+@pytest.mark.parametrize("hpar", ["1", "0"])
+def test_code_length_loops(hpar, monkeypatch):
+    """The dynamic header's code lengths: hdr_par's windows (default) and the
+    serial loop (BPMD_ZSTREAM_HPAR=0) against the oracle, under random cuts,
+    input a byte at a time, the KATs and corrupted headers."""
+    monkeypatch.setenv("BPMD_ZSTREAM_HPAR", hpar)
+    Z.case_connection_random_cuts(make, "json", 8, 4)
+    Z.case_byte_at_a_time_input(make)
+    Z.case_kat_split(make, every_cut=False)
+    Z.case_errors(make)
+
+
 def test_output_room_one_byte():
     Z.case_output_room_one_byte(make, n_calls=1500)
 
