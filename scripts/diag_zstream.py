@@ -58,7 +58,8 @@ def main():
     if c[27] + c[28] + c[29] + c[30]:   # switch trips by mode (nested laps included)
         print(f"  by mode: type {c[27] / k:.0f}, stored {c[28] / k:.0f}, dynamic header {c[29] / k:.0f}, "
               f"LEN..LIT {c[30] / k:.0f}, other {c[31] / k:.0f} cycles per message; "
-              f"{c[24] / k:.1f} slow-path symbols, {c[26] / k:.1f} block headers")
+              f"{c[24] / k:.1f} slow-path symbols, {c[25] / k:.1f} code-length symbols in hdr_par windows, "
+              f"{c[26] / k:.1f} block headers")
     if c[9]:
         print(f"  cycles per match copy {c[5] / c[9]:.0f}; per fast-loop token {c[3] / max(1, c[10]):.0f}")
     print("deflate (chunk kernel phases, per message):")
