@@ -920,6 +920,31 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
         return n;
     };
 
+    // ---- the code-length code's lengths (LENLENS) in one step when their bits
+    // are staged: lane j takes the 3 bits of length j; fill(3) one length at a
+    // time pulls ceil((first bit + 3 n) / 8) bytes in all, so ip / bn / bv
+    // are the serial loop's.  Otherwise (input short) the serial loop runs.
+    auto lenlens_par = [&]() {
+        const uint32_t* iw = (const uint32_t*)L.ist;
+        const uint64_t S = ip * 8 - bn;   // bn <= ip * 8
+        if ((S >> 3) < ib0 || (S >> 3) >= ib1 || (S >> 3) + ZSPAN > ib0 + IST) stage(S >> 3);
+        const uint32_t rb = (uint32_t)(S - 8 * ib0), nb = 3 * (h.ncode - h.have);
+        if (rb + nb > (uint32_t)(8 * (ib1 - ib0))) return;
+        wave_sync();
+        for (uint32_t j = h.have + lane; j < h.ncode; j += WAVE) {
+            const uint32_t r = rb + 3 * (j - h.have);
+            L.lens[kOrder[j]] = (uint8_t)(fsh(iw[(r >> 5) + 1], iw[r >> 5], r & 31) & 7u);
+        }
+        wave_sync();
+        const uint32_t rend = rb + nb, pulled = (rend + 7) & ~7u;
+        if (ib0 + (pulled >> 3) > ip) ip = ib0 + (pulled >> 3);
+        bn = (uint32_t)(ip - ib0) * 8 - rend;
+        const uint32_t v = fsh(uni(iw[(rend >> 5) + 1]), uni(iw[rend >> 5]), rend & 31);
+        bv = bn >= 32 ? v : v & ((1u << bn) - 1u);
+        h.have = h.ncode;
+        lens_dirty = true;
+    };
+
     int32_t ec = 0;
     int32_t published = 0;
     int32_t data_type = 0;
@@ -1025,6 +1050,7 @@ __device__ void zstream_run(Lds& L, State* __restrict__ st, const uint8_t* __res
             h.mode = LENLENS;
             [[fallthrough]];
         case LENLENS: {
+            if (hpar && h.have < h.ncode && bn <= ip * 8) lenlens_par();
             while (h.have < h.ncode) {
                 if (!fill(3)) goto done;
                 const uint32_t v = take(3);
