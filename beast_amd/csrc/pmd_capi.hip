@@ -104,6 +104,7 @@ struct Side {
 };
 std::mutex g_scratch_mu;
 std::vector<Scratch> g_scratch;
+std::vector<Scratch> g_pinned;   // small pinned host blocks per (device, stream), same lifetime rules
 std::vector<StreamLock> g_locks;
 std::vector<Side> g_sides;
 
@@ -188,6 +189,30 @@ extern "C" void* bpmd_internal_scratch(hipStream_t s, size_t bytes, int which)
     return scratch_for(s, bytes, which);
 }
 
+// A small pinned host block per (device, stream, which) -- the target of a
+// read-back that an event then covers (0: the deflate chunk count).  Kept
+// per stream, not per host thread: pmd_multi.hip launches each shard from a
+// thread of its own, and a thread_local block would leak one pinned
+// allocation per shard thread.  The caller holds the stream's
+// launch lock; freed by bpmd_internal_scratch_release.
+extern "C" void* bpmd_internal_pinned(hipStream_t s, size_t bytes, int which)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || bytes > 4096) return nullptr;
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    for (auto& e : g_pinned)
+        if (e.dev == dev && e.stream == s && e.which == which) return e.p;
+    uint8_t* p = nullptr;
+    if (hipHostMalloc((void**)&p, 4096, hipHostMallocDefault) != hipSuccess) return nullptr;
+    g_pinned.push_back(Scratch{dev, s, which, p, 4096});
+    return p;
+}
+extern "C" size_t bpmd_internal_pinned_count(void)
+{
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    return g_pinned.size();
+}
+
 // Frees every scratch block and the launch lock of a stream that is about to
 // be destroyed (per-stream codecs, batcher slots).  The caller has
 // synchronised the stream and no other thread uses it.
@@ -214,6 +239,15 @@ extern "C" void bpmd_internal_scratch_release(hipStream_t s)
             (void)hipFree(g_scratch[i].p);
             g_scratch[i] = g_scratch.back();
             g_scratch.pop_back();
+        } else {
+            ++i;
+        }
+    }
+    for (size_t i = 0; i < g_pinned.size();) {
+        if (g_pinned[i].dev == dev && (g_pinned[i].stream == s || (side && g_pinned[i].stream == side))) {
+            (void)hipHostFree(g_pinned[i].p);
+            g_pinned[i] = g_pinned.back();
+            g_pinned.pop_back();
         } else {
             ++i;
         }
@@ -439,7 +473,11 @@ int inflate_impl(const bpmd_cfg* cfg, const uint8_t* d_in, const uint64_t* d_in_
                     if (!side_for(s, sd) || hipEventRecord(sd.fork, s) != hipSuccess ||
                         hipStreamWaitEvent(sd.side, sd.fork, 0) != hipSuccess)
                         return BPMD_R_HIP_ERROR;
-                    // (both enqueue only: nothing here waits on the device)
+                    // (both enqueue only, except the stream's first
+                    // block-parallel call without bpmd_inflate_reserve: it
+                    // reads its workspace totals back once, on the side
+                    // stream, so it waits for the work queued before it --
+                    // and cannot run under stream capture)
                     const int eb = bpmd_internal_inflate_bp(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off,
                                                             d_out_cap, d_out_len, d_status, raw, order, nlong, sd.side);
                     e = bpmd_internal_inflate_lane3(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap,

@@ -1863,6 +1863,7 @@ stitch_kernel(const uint32_t* __restrict__ in_len, uint32_t n, uint32_t all, con
 
 extern "C" unsigned bpmd_diag_grid_override;
 extern "C" void* bpmd_internal_scratch(hipStream_t s, size_t bytes, int which);
+extern "C" void* bpmd_internal_pinned(hipStream_t s, size_t bytes, int which);
 #ifndef BPMD_DEFLATE_QUEUE
 #define BPMD_DEFLATE_QUEUE 1
 #endif
@@ -1952,9 +1953,10 @@ int deflate_impl(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_l
         const int e = all ? 0 : launch_single(in, in_off, in_len, n, out, out_off, out_cap, out_len, status, P, stream);
         if (e) return e;
     } else {
-    // a pinned word per host thread, so the copy is asynchronous and the event covers it
-    thread_local uint32_t* h_total = nullptr;
-    if (!h_total && hipHostMalloc((void**)&h_total, 64, hipHostMallocDefault) != hipSuccess) return (int)hipErrorOutOfMemory;
+    // a pinned word of the stream (the caller holds its launch lock), so the
+    // copy is asynchronous and the event covers it
+    uint32_t* h_total = (uint32_t*)bpmd_internal_pinned(stream, 64, 0);
+    if (!h_total) return (int)hipErrorOutOfMemory;
     hipEvent_t ev = nullptr;
     if ((he = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return (int)he;
     if ((he = hipMemcpyAsync(h_total, d_total, sizeof(uint32_t), hipMemcpyDeviceToHost, stream)) != hipSuccess ||

@@ -503,6 +503,10 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
                 // (this library's incompressible chunks go stored without a
                 // marker; Beast's binary payloads are 35-60 % stored blocks)
                 const uint32_t k = gl - task_base[ri], R = stats[ri].R;
+                // the region's real end: the last region also takes the
+                // payload's remainder (region_of), which may hold a block
+                // start past the stored block's data
+                const uint32_t rend = k + 1 == stats[ri].regions ? in_len[order[ri]] : (k + 1) * R;
                 bool inside = false;
                 for (uint32_t j = 1; j <= 8 && j <= k; ++j) {
                     const uint32_t kj = tasks[gl - j].kind;
@@ -512,7 +516,7 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
                     if (kj == KIND_STORED || (j == k && ((pm[0] >> 1) & 3u) == 0)) {
                         const uint32_t pb = kj == KIND_STORED ? tasks[gl - j].bit >> 3 : 1u;
                         const uint32_t d0 = pb + 4, d1 = d0 + ((uint32_t)pm[pb] | (uint32_t)pm[pb + 1] << 8);
-                        inside = d0 <= k * R && (k + 1) * R <= d1;
+                        inside = d0 <= k * R && rend <= d1;
                         break;
                     }
                     if (kj != KIND_PENDING && kj != KIND_NONE) break;
@@ -553,8 +557,11 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
                 const uint32_t q0 = ((s + k * st.R) >> 2) - 1;
                 const uint32_t nwords = STAGE_BYTES / 4 + 8;
                 const uint32_t tailm = ((s + len) & 3u) ? (1u << (8 * ((s + len) & 3u))) - 1u : ~0u;
-                // only the words this region's size needs are loaded
-                const uint32_t nw = (st.R + STAGE_EXTRA + 64) / 4 < nwords ? (st.R + STAGE_EXTRA + 64) / 4 : nwords;
+                // only the words this region's size needs are loaded (the last
+                // region also holds the payload's remainder, region_of: up to
+                // 1.5 R, searched as far as the stage holds it)
+                const uint32_t rlen = (k + 1 == st.regions ? len : (k + 1) * st.R) - k * st.R;
+                const uint32_t nw = (rlen + STAGE_EXTRA + 64) / 4 < nwords ? (rlen + STAGE_EXTRA + 64) / 4 : nwords;
                 {
                     // all loads in flight together (a load-store loop would
                     // wait out one memory latency per dword)
@@ -585,7 +592,8 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
                 const LdsBits Lb{S};
                 BP_DIAG(__builtin_amdgcn_s_waitcnt(0); const uint64_t t1 = __builtin_amdgcn_s_memtime());
                 const uint32_t b0 = 8 * k * st.R;                                     // region's first payload bit
-                const uint32_t b1 = 8 * (k + 1) * st.R < 8 * len ? 8 * (k + 1) * st.R : 8 * len;   // past its last
+                const uint32_t rs = 4 * nw - STAGE_EXTRA - 64 < rlen ? 4 * nw - STAGE_EXTRA - 64 : rlen;
+                const uint32_t b1 = 8 * (k * st.R + rs) < 8 * len ? 8 * (k * st.R + rs) : 8 * len;   // past its last
                 // 1. stored blocks, by their LEN / NLEN fields (a byte search
                 // over the whole region; this library's deflater writes an
                 // empty one before every chunk of a long message)
@@ -1456,6 +1464,12 @@ struct BpCaps {
     hipEvent_t ev;                     // recorded after that copy
     bool pending;                      // ev recorded, not yet consumed
     bool sized;                        // capacity set (first call or reserve)
+    // after a workspace allocation failed: the capacity that could be had is
+    // a ceiling for the next `hold` calls (8, doubling with every failure up
+    // to 1024), so under memory pressure a call does not sync, free and fail
+    // to allocate again every time
+    unsigned long long ceil_tasks, ceil_words;
+    uint32_t hold, backoff;
 };
 std::mutex g_bp_mu;
 std::vector<BpCaps> g_bp_caps;
@@ -1474,7 +1488,7 @@ BpCaps* caps_for(int dev, hipStream_t s)
 {
     for (auto& e : g_bp_caps)
         if (e.dev == dev && e.s == s) return &e;
-    BpCaps e{dev, s, 0, 0, nullptr, nullptr, false, false};
+    BpCaps e{dev, s, 0, 0, nullptr, nullptr, false, false, 0, 0, 0, 8};
     if (hipHostMalloc((void**)&e.seen, sizeof(bpmd::bp::Totals), hipHostMallocDefault) != hipSuccess) return nullptr;
     e.seen->tasks = e.seen->words = 0;
     if (hipEventCreateWithFlags(&e.ev, hipEventDisableTiming) != hipSuccess) {
@@ -1521,9 +1535,16 @@ void grow_to(BpCaps* c, unsigned long long t, unsigned long long w)
     if (nt > 0xffffffffull) nt = 0xffffffffull;
     size_t fr = 0, tot = 0;
     if ((nt != c->tasks || nw != c->words) && hipMemGetInfo(&fr, &tot) == hipSuccess) {
-        const unsigned long long budget = fr / 2, per_task = sizeof(bpmd::bp::SegTask) + sizeof(bpmd::bp::SegRes) + 4;
+        // per task: the task, its result, the region map word and the
+        // resolve's chain entries (DwLayout chp 4 B, chs 8 B)
+        const unsigned long long budget = fr / 2,
+                                 per_task = sizeof(bpmd::bp::SegTask) + sizeof(bpmd::bp::SegRes) + 4 + 4 + 8;
         if (nt * per_task > budget) nt = budget / per_task;
         if (2 * nw + nt * per_task > budget) nw = (budget - nt * per_task) / 2;
+    }
+    if (c->hold) {
+        nt = nt < c->ceil_tasks ? nt : c->ceil_tasks;
+        nw = nw < c->ceil_words ? nw : c->ceil_words;
     }
     c->tasks = nt > c->tasks ? nt : c->tasks;
     c->words = nw > c->words ? nw : c->words;
@@ -1586,6 +1607,7 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
         std::lock_guard<std::mutex> lk(g_bp_mu);
         BpCaps* c = caps_for(dev, s);
         if (!c) return (int)hipErrorOutOfMemory;
+        if (c->hold) --c->hold;   // the ceiling lifts after `hold` calls
         if (c->pending && hipEventQuery(c->ev) == hipSuccess) {
             c->pending = false;
             grow_to(c, c->seen->tasks, c->seen->words);
@@ -1684,6 +1706,10 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
         if (c) {
             c->tasks = cap_tasks;
             c->words = cap_words;
+            c->ceil_tasks = cap_tasks;
+            c->ceil_words = cap_words;
+            c->hold = c->backoff;
+            c->backoff = c->backoff < 1024 ? 2 * c->backoff : 1024u;
         }
     }
     const DwLayout D(cap_tasks, cap_words, n);
@@ -1778,6 +1804,26 @@ extern "C" void bpmd_diag_set_bp_skim(int on) { g_bp_skim.store(on ? 1 : 0); }
 
 // diagnostics (tests): the next k decode-workspace allocations fail
 extern "C" void bpmd_diag_bp_fail_alloc(int k) { g_bp_fail.store(k); }
+
+// diagnostics (tests): the stream's decode-workspace capacity and ceiling:
+// out[0] tasks, [1] words, [2] ceiling tasks, [3] ceiling words, [4] calls
+// the ceiling still holds; -1 when the stream has no entry
+extern "C" int bpmd_diag_bp_caps(hipStream_t s, unsigned long long* out5)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    std::lock_guard<std::mutex> lk(g_bp_mu);
+    for (auto& e : g_bp_caps)
+        if (e.dev == dev && e.s == s) {
+            out5[0] = e.tasks;
+            out5[1] = e.words;
+            out5[2] = e.ceil_tasks;
+            out5[3] = e.ceil_words;
+            out5[4] = e.hold;
+            return 0;
+        }
+    return -1;
+}
 
 extern "C" int bpmd_diag_bp_fallback(uint32_t* out8)
 {

@@ -146,9 +146,16 @@ int run_one(bpmd_stream* s, const uint8_t* in, size_t n, size_t out_cap, std::ve
     if (hn) std::memcpy(h + in_at, s->hist.data(), hn);
     if (n) std::memcpy(h + in_at + hn, in, n);
     uint8_t* d = s->dmem;
-    if (hipMemcpyAsync(d, h, sizeof m, hipMemcpyHostToDevice, s->hs) != hipSuccess) return BPMD_R_HIP_ERROR;
-    if (hn + n && hipMemcpyAsync(d + in_at, h + in_at, hn + n, hipMemcpyHostToDevice, s->hs) != hipSuccess)
+    // after the first copy from the pinned buffer is queued, every error
+    // return first waits for the stream: the next call refills (or frees)
+    // that buffer while the DMA could still read it
+    auto fail = [&]() {
+        (void)hipStreamSynchronize(s->hs);
         return BPMD_R_HIP_ERROR;
+    };
+    if (hipMemcpyAsync(d, h, sizeof m, hipMemcpyHostToDevice, s->hs) != hipSuccess) return fail();
+    if (hn + n && hipMemcpyAsync(d + in_at, h + in_at, hn + n, hipMemcpyHostToDevice, s->hs) != hipSuccess)
+        return fail();
     Meta* dm = (Meta*)d;
     // chunks of the chunk-parallel path: every chunk with a history window,
     // else only messages over one chunk (pmd_deflate.hip chunk_count)
@@ -157,8 +164,8 @@ int run_one(bpmd_stream* s, const uint8_t* in, size_t n, size_t out_cap, std::ve
                                                   &dm->out_cap, &dm->out_len, &dm->status, &dm->bits,
                                                   hn ? &dm->hist_len : nullptr, s->level, s->wbits, s->strategy,
                                                   s->tuned ? s->tune4 : nullptr, s->hs, chunks);
-    if (e) return BPMD_R_HIP_ERROR;
-    if (hipMemcpyAsync(h, d, out_at + out_cap, hipMemcpyDeviceToHost, s->hs) != hipSuccess) return BPMD_R_HIP_ERROR;
+    if (e) return fail();
+    if (hipMemcpyAsync(h, d, out_at + out_cap, hipMemcpyDeviceToHost, s->hs) != hipSuccess) return fail();
     if (hipStreamSynchronize(s->hs) != hipSuccess) return BPMD_R_HIP_ERROR;
     std::memcpy(&m, h, sizeof m);
     if (m.out_len > out_cap) return BPMD_R_HIP_ERROR;
@@ -520,7 +527,11 @@ extern "C" int bpmd_inflate_stream_write(bpmd_stream* s, bpmd_zparams* zs, int f
             ok = hipMemcpy((uint8_t*)zs->next_out + spec, s->dout + RES_AT + spec, res.out_used - spec,
                            hipMemcpyDeviceToHost) == hipSuccess;
     }
-    if (!ok) return BPMD_R_HIP_ERROR;   // the device state is unchanged only if the kernel never ran
+    if (!ok) {
+        // the pinned staging buffer may still be a DMA's source or target
+        (void)hipStreamSynchronize(hs);
+        return BPMD_R_HIP_ERROR;   // the device state is unchanged only if the kernel never ran
+    }
     if (res.published) {
         zs->next_in = (const uint8_t*)zs->next_in + res.in_used;
         zs->avail_in -= res.in_used;

@@ -131,57 +131,73 @@ def _cpu_model():
     return "unknown"
 
 
-def cpu_baselines(comp_buf, comp_off, comp_len, raw_lens, raw3, off3, len3, target_s=1.0):
-    """Host-core baselines on bounded samples of the C2 payloads (inflate)
-    and C3 messages (deflate, L6/mem4/w15 + pmd framing): the C restatement
-    of Beast's zlib ("port", byte-identical to Beast at L1-9) and the
-    reference's own zlib 1.3.1 ("reference", compiled from
-    test/extern/zlib-1.3.1 by oracle/Makefile) and, as an extra column, the
-    image's system zlib behind the same shim ("system"), each at 1 thread, 16
-    threads and T = 32 threads (the per-GPU share of an 8-GPU node's 256
-    hardware threads), capped at the cores this process may use.  Per
-    measurement the sample is sized for ~target_s of CPU work; median of 3,
-    outputs preallocated (oracle.time_batch)."""
-    from oracle import oracle as O
+CPU_REPS = 5   # median of 5 timed runs per measurement
+
+
+def _cpu_threads():
     cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    T = max(1, min(cores, 32))
-    T16 = max(1, min(cores, 16))
-    out = {"cpu_model": _cpu_model(), "nproc": os.cpu_count(), "cores_available": cores, "threads": T,
-           "threads_16": T16}
+    # T = 32: the per-GPU share of an 8-GPU node's 256 hardware threads,
+    # capped at the cores this process may use
+    return cores, max(1, min(cores, 32))
+
+
+def cpu_measure(impl, inflate, data, off, lens, caps, raw_bytes, threads, target_s=0.5, level=6, reps=CPU_REPS):
+    """One host-core measurement (oracle.time_batch: outputs preallocated, the
+    threads take contiguous message ranges): a probe of 64 messages on one
+    thread sizes a sample of ~target_s of work per thread; GiB/s of
+    uncompressed bytes, median of `reps` runs.  None when `impl` is absent."""
+    from oracle import oracle as O
+    n = len(lens)
+    probe = min(n, 64)
+    pr = O.time_batch(impl, inflate, data, off[:probe], lens[:probe], caps[:probe], threads=1, reps=1, level=level)
+    if pr is None:
+        return None
+    per_msg = max(pr[0] / probe, 1e-9)
+    k = int(min(n, max(probe, target_s / per_msg * threads)))
+    t, olen = O.time_batch(impl, inflate, data, off[:k], lens[:k], caps[:k], threads=threads, reps=reps, level=level)
+    gib = float(np.asarray(raw_bytes[:k], dtype=np.int64).sum()) / (1 << 30)
+    return {"value": round(gib / t, 4), "msgs": k, "seconds": round(t, 4), "out_len": olen}
+
+
+def cpu_baselines(comp_buf, comp_off, comp_len, raw_lens, raw3, off3, len3):
+    """Host-core baselines on bounded samples of the C2 payloads (inflate)
+    and C3 messages (deflate, L6/mem4/w15 + pmd framing).  Codecs: the
+    reference's own zlib 1.3.1 ("reference", compiled from
+    test/extern/zlib-1.3.1 by oracle/Makefile) -- Beast's zlib equals it at
+    levels 1-9, as the reference's own bench asserts
+    (test/bench/zlib/deflate_stream.cpp:147,168), and it is the faster of the
+    two, so it is the headline; the C restatement of Beast's zlib ("port",
+    oracle/) beside it; the image's system zlib ("system") as an extra
+    column.  1 thread and T = 32 threads; median of 5 per measurement."""
+    from oracle import oracle as O
+    cores, T = _cpu_threads()
+    out = {"cpu_model": _cpu_model(), "nproc": os.cpu_count(), "cores_available": cores, "threads": T}
     n = len(comp_len)
     ub = np.full(n, pmd.upper_bound(MSG_BYTES) + 16, dtype=np.uint32)
-
-    def leg(impl, inflate, threads):
-        probe_n = min(n, 256)
-        args = (comp_buf, comp_off, comp_len, raw_lens) if inflate else (raw3, off3, len3, ub)
-        pr = O.time_batch(impl, inflate, args[0], args[1][:probe_n], args[2][:probe_n], args[3][:probe_n],
-                          threads=1, reps=1)
-        if pr is None:
-            return None
-        per_msg = max(pr[0] / probe_n, 1e-9)
-        k = int(min(n, max(probe_n, target_s / per_msg * threads)))
-        t, olen = O.time_batch(impl, inflate, args[0], args[1][:k], args[2][:k], args[3][:k], threads=threads)
-        gib = float(k * MSG_BYTES) / (1 << 30)
-        return {"value": round(gib / t, 4), "msgs": k, "seconds": round(t, 4), "out_len": olen}
-
+    raw_c2 = np.full(n, MSG_BYTES, dtype=np.int64)
     for name, inflate in (("inflate", True), ("deflate", False)):
+        args = (comp_buf, comp_off, comp_len, raw_lens) if inflate else (raw3, off3, len3, ub)
         r = {}
-        for impl in ("port", "reference", "system"):
-            one = leg(impl, inflate, 1)
-            many = leg(impl, inflate, T) if one else None
-            mid = leg(impl, inflate, T16) if one and T16 != T else many
-            if one:
-                r[impl] = {"1_thread": one["value"], f"{T16}_threads": mid["value"], f"{T}_threads": many["value"],
-                           "sample_1": f"{one['msgs']} msgs", f"sample_{T}": f"{many['msgs']} msgs"}
-                if not inflate and impl == "port":
-                    r["_beast_len"] = many["out_len"]
+        for impl, ths in (("reference", (1, T)), ("port", (1, T)), ("system", (T,))):
+            row = {}
+            for th in ths:
+                m = cpu_measure(impl, inflate, *args, raw_c2, th)
+                if m is None:
+                    break
+                row[f"{th}_threads"] = m["value"]
+                row[f"sample_{th}"] = f"{m['msgs']} msgs"
                 if inflate:   # the sample decodes exactly (every message is 4096 bytes)
-                    r[impl]["exact"] = bool((one["out_len"] == MSG_BYTES).all())
+                    row["exact"] = bool(row.get("exact", True) and (m["out_len"] == MSG_BYTES).all())
+                if not inflate and impl == "port" and th == T:
+                    r["_beast_len"] = m["out_len"]   # the port = Beast's deflate: sizes for size_vs_beast
+            if row:
+                r[impl] = row
         if "system" in r:
             r["system"]["version"] = O.zsys().zref_version().decode()
         if "port" in r and "reference" in r:
-            # calibration: per-byte time of the port relative to zlib 1.3.1 on one core
-            r["t_port_over_t_zlib_1thread"] = round(r["reference"]["1_thread"] / r["port"]["1_thread"], 3)
+            # per-byte time of the port relative to zlib 1.3.1, one core and T threads
+            r["t_port_over_t_zlib_1thread"] = round(r["reference"]["1_threads"] / r["port"]["1_threads"], 3)
+            r[f"t_port_over_t_zlib_{T}threads"] = round(r["reference"][f"{T}_threads"] / r["port"][f"{T}_threads"], 3)
         out[name] = r
     return out
 
@@ -435,6 +451,27 @@ def mixed_legs(args, rank, world, timer, dev):
             bsrc = pmd.Batch(torch.from_numpy(bbuf).to(dev), torch.from_numpy(boff).to(dev),
                              torch.from_numpy(blen).to(dev))
             bcomp = int(blen.astype(np.int64).sum())
+            if rank == 0 and world == 1 and not args.no_cpu_baseline:
+                # the leg on the host cores (reference/test/bench/zlib/
+                # inflate_stream.cpp:100-125 times Beast's and zlib's inflate
+                # of the same payloads): zlib 1.3.1 (= Beast) at T threads,
+                # inflate of the Beast payloads, deflate of the messages at the
+                # leg's level; bounded samples, median of 5
+                _, T = _cpu_threads()
+                hcap = hln.astype(np.uint32)
+                ci = cpu_measure("reference", True, bbuf, boff.astype(np.uint64), blen.astype(np.uint32), hcap, hln,
+                                 T, level=level)
+                dub = (hln.astype(np.int64) + (hln.astype(np.int64) + 7) // 8 + (hln.astype(np.int64) + 63) // 64
+                       + 16).astype(np.uint32)
+                cd = cpu_measure("reference", False, hraw, hoff.astype(np.uint64), hln.astype(np.uint32), dub, hln, T,
+                                 level=level)
+                if ci and cd:
+                    out[name]["cpu_baseline"] = {
+                        "kind": "reference", "codec": "zlib 1.3.1 (reference/test/extern, = Beast's zlib)",
+                        "cores": T, "unit": "GiB/s", "inflate": ci["value"], "deflate": cd["value"],
+                        "inflate_exact": bool((ci["out_len"] == hln[:ci["msgs"]]).all()),
+                        "sample": f"inflate {ci['msgs']} / deflate {cd['msgs']} of the leg's messages "
+                                  f"(Beast payloads for inflate), median of {CPU_REPS}"}
             del bbuf
 
             def beast_step(a=0, b=len(lens)):
@@ -481,6 +518,66 @@ def mixed_legs(args, rank, world, timer, dev):
             del bsrc, rb
         del cbuf, rbuf, comp, d, r
     return out
+
+
+def compact_line(full):
+    """The bench's stdout line: the contract's keys, the C2 roofline and CPU
+    baseline, and every north-star number (C3 deflate and size, C4 / C5
+    deflate, inflate of this library's and of a Beast peer's payloads, the
+    projected 2 / 4 / 8-way speed-ups, the legs' CPU columns, parity).  The
+    whole record goes to gpurun_out/bench_detail.json."""
+    keys = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config", "parity_ok")
+    line = {k: full[k] for k in keys if k in full}
+    rf = dict(full["roofline"])
+    src = rf.pop("traffic_source", None)
+    rf["traffic_source"] = src.get("source") if isinstance(src, dict) else src
+    line["roofline"] = rf
+    cb = full.get("cpu_baseline")
+    if cb:
+        line["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample", "one_thread")}
+        line["cpu_baseline"]["port_value"] = (cb.get("port") or {}).get("value")
+        line["cpu_baseline"]["cpu_model"] = cb.get("cpu_model")
+    ns = {"c2_inflate": full["value"]}
+    ok = [bool(full.get("parity_ok"))]
+    d = full.get("deflate")
+    if d:
+        ns["c3"] = {"deflate": d["deflate_value"], "roundtrip": d["roundtrip_value"],
+                    "inflate_own": d["inflate_of_gpu_payloads_value"], "size_vs_beast": d.get("size_vs_beast"),
+                    "deflate_frac": d["roofline"]["frac"],
+                    "exact_deflate": (d.get("exact") or {}).get("deflate_value"),
+                    "exact_same_size": (d.get("exact") or {}).get("same_size_as_beast"),
+                    "cpu_deflate": (d.get("cpu_baseline") or {}).get("value")}
+        ok.append(bool(d["roundtrip_ok"]))
+    fr = full.get("frame")
+    if fr:
+        ns["n1"] = {"read": fr["read_value"], "utf8": fr["utf8_value"], "mask": fr["mask_value"],
+                    "frame": fr["frame_value"]}
+        ok += [bool(fr["read_ok"]), bool(fr["utf8_ok"]), bool(fr["frame_ok"])]
+    for leg, m in (full.get("mixed") or {}).items():
+        if not isinstance(m, dict) or "deflate_value" not in m:
+            continue
+        e = {"deflate": m["deflate_value"], "inflate": m["inflate_value"], "inflate_beast": m.get("inflate_beast_value"),
+             "ratio": m["ratio_rank_local"], "beast_ratio": m.get("beast_ratio_rank_local"),
+             "inflate_frac": m["inflate_roofline"]["frac"], "deflate_frac": m["deflate_roofline"]["frac"]}
+        if m.get("beast_ratio_rank_local"):
+            e["size_vs_beast"] = round(m["ratio_rank_local"] / m["beast_ratio_rank_local"], 4)
+        vs = m.get("virtual_shards")
+        if vs:
+            # projected N-GPU speed-ups, N = 2, 4, 8: [deflate, inflate, inflate of Beast payloads]
+            e["x_projected"] = {n: [v.get("deflate_projected_speedup"), v.get("inflate_projected_speedup"),
+                                    v.get("inflate_beast_projected_speedup")] for n, v in vs.items()}
+            e["shard8_ms_max"] = [max(vs["8"]["deflate_shard_ms"]), max(vs["8"]["inflate_shard_ms"]),
+                                  max(vs["8"].get("inflate_beast_shard_ms") or [0])]
+        if m.get("cpu_baseline"):
+            e["cpu"] = {"inflate": m["cpu_baseline"]["inflate"], "deflate": m["cpu_baseline"]["deflate"],
+                        "cores": m["cpu_baseline"]["cores"]}
+        ns[leg] = e
+        ok += [bool(m["roundtrip_ok"]), bool(m.get("inflate_beast_ok", True))]
+    line["parity_ok"] = all(ok)
+    line["north_star"] = ns
+    line["detail"] = "gpurun_out/bench_detail.json"
+    return line
 
 
 def launch_cmd(argv, n, port, python=sys.executable, script=None):
@@ -761,13 +858,13 @@ def main():
                 if exact_len is not None:
                     result["deflate"]["exact"]["same_size_as_beast"] = f"{int((exact_len[:k] == beast_len).sum())}/{k}"
                 result["deflate"]["size_sample"] = f"first {k} messages, Σ GPU bytes / Σ Beast bytes at L6/mem4"
-            if "port" in dcpu:
+            if "reference" in dcpu:
                 T = cpu["threads"]
                 result["deflate"]["cpu_baseline"] = {
-                    "value": dcpu["port"][f"{T}_threads"], "unit": "GiB/s", "cores": T, "kind": "port",
-                    "value_16_threads": dcpu["port"][f"{cpu['threads_16']}_threads"],
-                    "sample": f"C3 messages, {dcpu['port'][f'sample_{T}']}, L6/mem4/w15 + pmd framing",
-                    "one_thread": dcpu["port"]["1_thread"], "reference_zlib_1.3.1": dcpu.get("reference"),
+                    "value": dcpu["reference"][f"{T}_threads"], "unit": "GiB/s", "cores": T, "kind": "reference",
+                    "sample": f"C3 messages, {dcpu['reference'][f'sample_{T}']}, L6/mem4/w15 + pmd framing, "
+                              f"zlib 1.3.1 (= Beast), median of {CPU_REPS}",
+                    "one_thread": dcpu["reference"]["1_threads"], "port": dcpu.get("port"),
                     "system_zlib": dcpu.get("system")}
         del src3, out3, rt_out, d, rr
 
@@ -780,18 +877,28 @@ def main():
             cpu = cpu_baselines(comp_buf, comp_off, comp_len, raw_len.astype(np.uint32), raw, raw_off, raw_len)
         icpu = cpu["inflate"]
         T = cpu["threads"]
-        if "port" in icpu:
+        if "reference" in icpu:
+            ref_, port_ = icpu["reference"], icpu.get("port") or {}
             result["cpu_baseline"] = {
-                "value": icpu["port"][f"{T}_threads"], "unit": "GiB/s", "cores": T, "kind": "port",
-                "value_16_threads": icpu["port"][f"{cpu['threads_16']}_threads"],
-                "sample": f"C2 payloads, {icpu['port'][f'sample_{T}']} x {MSG_BYTES} B, oracle inflate "
-                          f"(C restatement of Beast's zlib), {T} threads, median of 3",
-                "one_thread": icpu["port"]["1_thread"], "reference_zlib_1.3.1": icpu.get("reference"),
-                "system_zlib": icpu.get("system"),
-                "t_port_over_t_zlib_1thread": icpu.get("t_port_over_t_zlib_1thread"),
+                "value": ref_[f"{T}_threads"], "unit": "GiB/s", "cores": T, "kind": "reference",
+                "sample": f"C2 payloads, {ref_[f'sample_{T}']} x {MSG_BYTES} B, zlib 1.3.1 of the reference "
+                          f"(oracle/_ref; = Beast's zlib), {T} threads, median of {CPU_REPS}",
+                "one_thread": ref_["1_threads"], "exact": ref_.get("exact"),
+                "port": {"value": port_.get(f"{T}_threads"), "one_thread": port_.get("1_threads"),
+                         "t_port_over_t_zlib_1thread": icpu.get("t_port_over_t_zlib_1thread"),
+                         f"t_port_over_t_zlib_{T}threads": icpu.get(f"t_port_over_t_zlib_{T}threads")},
+                "system_zlib": (icpu.get("system") or {}).get(f"{T}_threads"),
                 "cpu_model": cpu["cpu_model"], "nproc": cpu["nproc"], "cores_available": cpu["cores_available"]}
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        # the whole record to a side file; stdout gets one line under ~4 KB
+        # with every north-star number (the driver keeps only a tail of it)
+        try:
+            os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+            with open(os.path.join(ROOT, "gpurun_out", "bench_detail.json"), "w") as fh:
+                json.dump(result, fh)
+        except OSError:
+            pass
+        print(json.dumps(compact_line(result)), flush=True)
     if dist:
         dist.destroy_process_group()
 

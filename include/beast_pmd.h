@@ -32,7 +32,9 @@
  *   - the first inflate call on a stream that decodes long payloads
  *     block-parallel reads back that batch's workspace totals once (so the
  *     first call already runs the fast path), unless bpmd_inflate_reserve()
- *     sized the stream before.
+ *     sized the stream before.  That read-back waits for the work queued on
+ *     the stream before the call, so a stream that is being captured into a
+ *     graph (hipStreamBeginCapture) must be reserved first.
  * Concurrent calls from several host threads on one stream are serialised
  * per stream.
  */

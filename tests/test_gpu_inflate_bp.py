@@ -245,6 +245,53 @@ def test_foreign_payload_with_one_early_flush():
     assert c[0] == 4 and c[1] >= 4 * 16 and c[2] == 0, list(c)[:4]
 
 
+
+def test_stored_block_ending_in_the_last_region():
+    """the last region of a payload also takes the remainder past
+    regions * R (region_of), so a stored block whose data ends inside it, past
+    (k + 1) * R, may be followed by a block start in that region.  Pass 2 used
+    to take (k + 1) * R as the region's end (skipping it as "inside the stored
+    data") and searched only up to there; it now uses the real end, and the
+    dynamic block after the stored data becomes a segment of its own.  Payload:
+    17 hand-made stored blocks (random bytes) ending in the last region, then a
+    small dynamic block (CPython zlib, BFINAL 0, sync-flushed; the pmd tail is
+    stripped).  Exact output, 18 segments per payload (the start, 16 stored
+    blocks found by pass 1, the dynamic block)."""
+    import ctypes
+    import zlib
+    pmd = _pmd()
+    R = 1024   # R_MIN: four ~68 KB payloads are far below a lane's share
+    js = _data("json", 700, 11)
+    co = zlib.compressobj(6, zlib.DEFLATED, -15, 4)
+    dyn = co.compress(js) + co.flush(zlib.Z_SYNC_FLUSH)
+    assert dyn.endswith(b"\x00\x00\xff\xff") and (dyn[0] >> 1) & 3 == 2 and not dyn[0] & 1
+    dyn = dyn[:-4]
+    D = len(dyn)
+    assert D < R // 2 - 16
+    K = 66   # regions: round((S + D) / R) == K, stored data ending past K * R
+    S = K * R + 8
+    rnd = random.Random(5)
+    sizes = [4000] * 16
+    sizes.append(S - sum(sizes) - 5 * 17)
+    stored, plain = b"", b""
+    for n in sizes:
+        blk = bytes(rnd.getrandbits(8) for _ in range(n))
+        stored += b"\x00" + n.to_bytes(2, "little") + (n ^ 0xFFFF).to_bytes(2, "little") + blk
+        plain += blk
+    assert len(stored) == S and round((S + D) / R) == K
+    p = stored + dyn
+    payloads = [p] * 4
+    c = (ctypes.c_ulonglong * 12)()
+    pmd.lib().bpmd_diag_bp_counters(c, 1)
+    assert pmd.lib().bpmd_set_inflate_kernel(3) == 0
+    try:
+        _check(payloads, len(plain) + len(js) + 16)
+    finally:
+        pmd.lib().bpmd_set_inflate_kernel(0)
+    pmd.lib().bpmd_diag_bp_counters(c, 1)
+    assert c[0] == 4 and c[1] == 4 * 18 and c[2] == 0, list(c)[:4]
+
+
 # ---------------------------------------------------- workspace sizing (r05)
 # A stream's block-parallel decode workspace is sized on its first call (one
 # read-back) or by bpmd_inflate_reserve; payloads over the capacity are
@@ -321,11 +368,20 @@ def test_reserved_too_small_spills_then_grows():
 
 def test_failed_workspace_allocation_falls_back():
     """The first three decode-workspace allocations fail: the call keeps a
-    smaller workspace (exact output, spills to the wave kernel), and the next
-    call on the same stream grows it again and decodes everything
-    block-parallel."""
+    smaller workspace (exact output, spills to the wave kernel).  That
+    capacity is then a ceiling for the next 8 calls (under memory
+    pressure every call would otherwise sync, free and fail again): the two
+    calls after it keep the same capacity -- no regrowth, so no allocation
+    and no stream sync -- and spill exactly; once the hold has run out the
+    capacity grows again and every payload decodes block-parallel."""
+    import ctypes
     src, comp, cap = _c5_like(2048, 0x5EED0063)
     pmd = _pmd()
+
+    def caps(st):
+        v = (ctypes.c_ulonglong * 5)()
+        assert pmd.lib().bpmd_diag_bp_caps(ctypes.c_void_p(st.cuda_stream), v) == 0
+        return list(v)
 
     def body(st):
         pmd.lib().bpmd_diag_bp_fail_alloc(3)
@@ -334,6 +390,17 @@ def test_failed_workspace_allocation_falls_back():
         finally:
             pmd.lib().bpmd_diag_bp_fail_alloc(0)
         assert ok and c[3] > 0, c[:4]
+        c0 = caps(st)
+        assert c0[0] == c0[2] and c0[1] == c0[3] and c0[4] == 8, c0
+        for k in range(2):
+            ok, c = _call(st, comp, cap, src)
+            assert ok and c[3] > 0, c[:4]
+            ck = caps(st)
+            assert ck[:4] == c0[:4] and ck[4] == 7 - k, (ck, c0)
+        for _ in range(7):
+            ok, c = _call(st, comp, cap, src)
+            assert ok
+        assert caps(st)[4] == 0
         ok, c = _call(st, comp, cap, src)
         assert ok and c[0] == 2048 and c[3] == 0, c[:4]
     _on_fresh_stream(body)

@@ -62,3 +62,27 @@ def test_multi_rejects_bad_device():
     cfg = pmd._Cfg(6, 15, 4, 0, 0)
     assert L.bpmd_inflate_batch_multi(ctypes.byref(cfg), arr, 1, None) == -1
     assert L.bpmd_deflate_batch_multi(ctypes.byref(cfg), arr, 1, None) == -1
+
+
+def test_multi_deflate_pinned_memory_flat():
+    """every shard runs on a host thread of its own, and the chunk
+    count's pinned read-back word used to be thread_local, i.e. one pinned
+    allocation leaked per shard thread and call.  It is now one word per
+    (device, stream): repeated multi-shard deflates of long messages keep the
+    count of pinned blocks flat."""
+    import ctypes
+    L = pmd.lib()
+    L.bpmd_internal_pinned_count.restype = ctypes.c_size_t
+    lens = np.full(64, 20000, dtype=np.uint32)   # > 4 KiB: the chunk-count read-back runs
+    data, off, ln = synth.make_batch("json", lens, seed=0x5EED00A2)
+    src = pmd.Batch.from_arrays(data, off, ln)
+    ranges = pmd.shard_ranges(lens, 4)
+    streams = [torch.cuda.Stream() for _ in ranges]
+    pmd.deflate_batch_multi([_sub(src, a, e) for a, e in ranges], level=6, streams=streams)
+    torch.cuda.synchronize()
+    base = L.bpmd_internal_pinned_count()
+    for _ in range(5):
+        dres, _tot = pmd.deflate_batch_multi([_sub(src, a, e) for a, e in ranges], level=6, streams=streams)
+        torch.cuda.synchronize()
+        assert all(int((r.status != 0).sum()) == 0 for r in dres)
+    assert L.bpmd_internal_pinned_count() == base
