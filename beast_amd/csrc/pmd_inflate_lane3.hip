@@ -175,12 +175,18 @@ constexpr uint32_t W_HIST = O_HIST / 4, W_LE = O_LE / 4, W_NIB = O_NIB / 4, W_HE
 // [0] decoder cycles [1] decoder iterations [2] decoder sleeps [3] decoder
 // header iterations [4] expander cycles [5] expander iterations [6] expander sleeps
 __device__ unsigned long long g_l3prof[16];
+// [0-4] decoder cycles in the header section's parts (type / stored / copy,
+// TABLE + LENLENS, CODELENS, BUILD, PLACE), [5-7] spare (prof build only)
+__device__ unsigned long long g_l3hprof[8];
 #ifdef BPMD_PROF
 #define L3_DECL unsigned long long l3t0_ = __builtin_amdgcn_s_memtime(), l3c_[4] = {0, 0, 0, 0}
 #define L3_CNT(i) (l3c_[i] += 1)
 #define L3_LAPDECL unsigned long long l3l_ = __builtin_amdgcn_s_memtime(), l3lap_[4] = {0, 0, 0, 0}
 #define L3_LAP(i) do { const unsigned long long t2_ = __builtin_amdgcn_s_memtime(); l3lap_[i] += t2_ - l3l_; l3l_ = t2_; } while (0)
-#define L3_LAPFLUSH() do { if ((threadIdx.x & 63) == 0) for (int i_ = 0; i_ < 4; ++i_) atomicAdd(&g_l3prof[8 + i_], l3lap_[i_]); } while (0)
+#define L3_LAPFLUSH() do { if ((threadIdx.x & 63) == 0) { for (int i_ = 0; i_ < 4; ++i_) atomicAdd(&g_l3prof[8 + i_], l3lap_[i_]); \
+    for (int i_ = 0; i_ < 5; ++i_) atomicAdd(&g_l3hprof[i_], l3h_[i_]); } } while (0)
+#define L3_HSTART() unsigned long long l3hl_ = __builtin_amdgcn_s_memtime()
+#define L3_HLAP(i) do { const unsigned long long t2_ = __builtin_amdgcn_s_memtime(); l3h_[i] += t2_ - l3hl_; l3hl_ = t2_; } while (0)
 #define L3_FLUSH(base) do { if ((threadIdx.x & 63) == 0) { atomicAdd(&g_l3prof[base], __builtin_amdgcn_s_memtime() - l3t0_); \
     for (int i_ = 1; i_ < 4; ++i_) atomicAdd(&g_l3prof[base + i_], l3c_[i_]); } } while (0)
 #else
@@ -190,6 +196,8 @@ __device__ unsigned long long g_l3prof[16];
 #define L3_LAPDECL
 #define L3_LAP(i)
 #define L3_LAPFLUSH()
+#define L3_HSTART()
+#define L3_HLAP(i)
 #endif
 
 static __constant__ const uint8_t kClenOrder2[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
@@ -1042,7 +1050,7 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
     L3_DECL;
     L3_LAPDECL;
 #ifdef BPMD_PROF
-    unsigned long long l3x_[4] = {0, 0, 0, 0}, l3dyn_ = 0;
+    unsigned long long l3x_[4] = {0, 0, 0, 0}, l3dyn_ = 0, l3h_[5] = {0, 0, 0, 0, 0};
 #endif
 
     for (;;) {
@@ -1104,6 +1112,7 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
         // is in a block's data or finished: a wave issues every instruction
         // of the section's per-state tests otherwise, exec-mask work included)
         if (__ballot(st0 != S_DATA && st0 != S_DONE)) {
+        L3_HSTART();
         if (SEG && st == S_TYPE && st0 == S_TYPE && !last) {
             // a block boundary: the next candidate's header starts here, or
             // candidates this segment has passed (not headers) are dropped
@@ -1268,6 +1277,7 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
         // ================================================== D. dynamic header
         // the code-length scratch shares LDS with the token ring: a dynamic
         // header starts once the expander has taken every entry
+        L3_HLAP(0);
         if (st == S_DYN && ring_empty) {
             // TABLE / LENLENS (inflate_stream.ipp:222-262)
             refill();
@@ -1340,6 +1350,7 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
                 }
             }
         }
+        L3_HLAP(1);
 #pragma unroll
         for (int kc = 0; kc < KCL; ++kc) {
             if (st != S_PASS1 || st0 != S_PASS1) break;
@@ -1412,6 +1423,7 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
                     }
                 }
         }
+        L3_HLAP(2);
         if (st == S_BUILD) {
             if (!eob_seen) {
                 result = ST_MISSING_EOB;
@@ -1460,6 +1472,7 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
                 }
             }
         }
+        L3_HLAP(3);
         if (st == S_PASS2) {
             // place symbols in canonical order (inflate_stream.ipp:632-640)
 #pragma unroll
@@ -1489,6 +1502,7 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
             if (have >= want) st = S_DATA;
         }
 
+        L3_HLAP(4);
         }   // block headers, stored
         L3_LAP(2);
         // ---- publish the token (entry first, then head)
@@ -1774,16 +1788,22 @@ extern "C" const uint32_t* bpmd_internal_lane_long_split(const uint32_t* in_len,
     return (const uint32_t*)split + 2;
 }
 
-// diagnostic counters of the pipelined lane kernel (meaningful only in the -DBPMD_PROF build)
-extern "C" int bpmd_diag_lane3_counters(unsigned long long* out8, int reset)
+// diagnostic counters of the pipelined lane kernel (meaningful only in the
+// -DBPMD_PROF build): out[0-15] g_l3prof, out[16-23] g_l3hprof when `out` has
+// 24 entries (n24 != 0)
+static int lane3_counters(unsigned long long* out, int reset, int n24)
 {
     hipError_t e = hipDeviceSynchronize();
     if (e != hipSuccess) return (int)e;
-    e = hipMemcpyFromSymbol(out8, HIP_SYMBOL(bpmd::lp3::g_l3prof), sizeof(unsigned long long) * 16);
+    e = hipMemcpyFromSymbol(out, HIP_SYMBOL(bpmd::lp3::g_l3prof), sizeof(unsigned long long) * 16);
+    if (e == hipSuccess && n24) e = hipMemcpyFromSymbol(out + 16, HIP_SYMBOL(bpmd::lp3::g_l3hprof), sizeof(unsigned long long) * 8);
     if (e != hipSuccess) return (int)e;
     if (reset) {
         unsigned long long z[16] = {0};
         e = hipMemcpyToSymbol(HIP_SYMBOL(bpmd::lp3::g_l3prof), z, sizeof z);
+        if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(bpmd::lp3::g_l3hprof), z, sizeof(unsigned long long) * 8);
     }
     return (int)e;
 }
+extern "C" int bpmd_diag_lane3_counters(unsigned long long* out16, int reset) { return lane3_counters(out16, reset, 0); }
+extern "C" int bpmd_diag_lane3_counters24(unsigned long long* out24, int reset) { return lane3_counters(out24, reset, 1); }

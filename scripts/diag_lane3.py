@@ -25,18 +25,19 @@ def main():
     src = pmd.Batch(torch.from_numpy(buf).to(dev), torch.from_numpy(coff).to(dev), torch.from_numpy(clen).to(dev))
     cap = torch.full((n,), size, dtype=torch.int32, device=dev)
     L = pmd.lib()
-    c = (ctypes.c_ulonglong * 16)()
+    c = (ctypes.c_ulonglong * 24)()
     pmd.inflate_batch(src, cap)
     torch.cuda.synchronize()
-    L.bpmd_diag_lane3_counters(c, 1)
+    L.bpmd_diag_lane3_counters24(c, 1)
     r = pmd.inflate_batch(src, cap)
     torch.cuda.synchronize()
-    L.bpmd_diag_lane3_counters(c, 1)
+    L.bpmd_diag_lane3_counters24(c, 1)
     ok = torch.equal(r.out.data[: n * size].view(n, size), torch.from_numpy(raw.reshape(n, size)).to(dev))
     w = n // 64
     names = ["dec cycles", "dec iters", "dec sleeps", "dec hdr iters", "exp cycles", "exp iters", "exp sleeps", "lanes: header, ring not empty",
              "dec lap: input+tail", "dec lap: S_DATA", "dec lap: headers", "dec lap: publish+loop",
-             "lanes: data, ring full", "lanes: data, room", "lanes: finished", "lanes: in headers"]
+             "lanes: data, ring full", "lanes: data, room", "lanes: finished", "lanes: in headers",
+             "hdr: type/stored/copy", "hdr: table+lenlens", "hdr: codelens", "hdr: build", "hdr: place", "-", "-", "-"]
     for i, nm in enumerate(names):
         if nm == "-":
             continue
