@@ -161,6 +161,17 @@ LZ_HD bool incompressible(unsigned hits, unsigned chunk_bytes)
 {
     return INCOMP_DEN && (unsigned long long)hits * INCOMP_STRIDE * INCOMP_DEN < chunk_bytes;
 }
+// Round 6: an incompressible chunk of a message longer than one chunk is a
+// stored block outright (no parse, no trees).  A Huffman code over near-random
+// bytes saved ~0.7 % of them (C5: 0.9932 of the input; stored: ~1.0001), and a
+// stored block inflates as one copy: the block-parallel decoder takes it as a
+// single token and a lane never decodes it symbol by symbol -- C5's 8-way
+// shards were one Huffman chunk's serial decode.  Messages of one
+// chunk keep the size-based choice.  0 restores round 5's rule.
+#ifndef BPMD_INCOMP_STORED
+#define BPMD_INCOMP_STORED 1
+#endif
+constexpr bool INCOMP_STORED = BPMD_INCOMP_STORED != 0;
 
 LZ_HD uint32_t chain_hash(uint32_t w, unsigned avail, unsigned hbits)
 {

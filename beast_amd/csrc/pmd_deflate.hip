@@ -925,6 +925,10 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
             }
         }
         pf.lap(1);
+        if (INCOMP_STORED && no_parse && len > CHUNK) {
+            kind = 0;   // stored outright (lz_core.h INCOMP_STORED)
+            goto emit_block;
+        }
         [[maybe_unused]] unsigned steps = 0, finds = 0, iters = 0;
         // ---- parse (head table dead from here; tok[] reuses it)
         unsigned seg = (clen + WAVE - 1) / WAVE;
@@ -1271,6 +1275,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
         pf.lap(10);
     }
 
+emit_block:
     if (kind == 0) {
         // ---- stored block: 000, pad, LEN, NLEN, bytes (tr_stored_block)
         const unsigned hb = o.cbits + 3 > 8 ? 2u : 1u;

@@ -350,6 +350,50 @@ __device__ bool dyn_header_ok(const Bits& B, uint32_t b, uint32_t lim)
     return true;
 }
 
+// Could a fixed-code block start at bit b?  BFINAL 0, BTYPE 1, then the
+// first FW symbols of the fixed code (inflate_stream.ipp:865-930; RFC 1951
+// 3.2.6) decoded arithmetically: no end of block among them (a Beast peer cuts
+// a block every lit_bufsize - 1 = 1 023 symbols, deflate_stream.ipp:1406),
+// no invalid literal/length (286, 287) or distance (30, 31) code, and at most
+// FMAX length codes.  Random bits decode as ~22 % length codes (the 7-bit
+// codes 257-279 and 8-bit 280-285), the near-random data a Beast peer codes
+// in fixed blocks as 0-5 % (C5: tr_flush_block picks fixed for it,
+// deflate_stream.ipp:1425-1518): the test tells a real block start from the
+// ~8 random offsets per KiB that show a fixed header after seven zero bits
+// (a fixed block's end-of-block code).  A block it rejects -- a fixed block
+// of text with many matches, say -- is only not a segment start.
+constexpr uint32_t FW = 48, FMAX = 4;
+template <class Bits>
+__device__ bool fixed_block_ok(const Bits& B, uint32_t b, uint32_t lim)
+{
+    if (b + 3 + FW * 9 > lim) return false;
+    if ((B.peek(b) & 7u) != 2u) return false;   // BFINAL 0, BTYPE 1
+    uint32_t p = b + 3, nm = 0;
+    for (uint32_t k = 0; k < FW; ++k) {
+        if (p + 32 > lim) return false;
+        const uint32_t v = B.peek(p);
+        const uint32_t c9 = __builtin_bitreverse32(v) >> 23;   // the next 9 code bits, first bit highest
+        const uint32_t c7 = c9 >> 2, c8 = c9 >> 1;
+        uint32_t sym, len;
+        if (c7 <= 23u) { sym = 256u + c7; len = 7; }
+        else if (c8 >= 48u && c8 <= 191u) { sym = c8 - 48u; len = 8; }
+        else if (c8 >= 192u && c8 <= 199u) { sym = 280u + c8 - 192u; len = 8; }
+        else { sym = 144u + c9 - 400u; len = 9; }
+        if (sym == 256u || sym > 285u) return false;
+        p += len;
+        if (sym > 256u) {
+            if (++nm > FMAX) return false;
+            const uint32_t li = sym - 257u;
+            const uint32_t xl = (li < 8u || li == 28u) ? 0u : ((li - 4u) >> 2);
+            const uint32_t v2 = B.peek(p + xl);
+            const uint32_t d5 = __builtin_bitreverse32(v2) >> 27;
+            if (d5 >= 30u) return false;
+            p += xl + 5u + (d5 < 4u ? 0u : (d5 >> 1) - 1u);
+        }
+    }
+    return true;
+}
+
 // Kraft sum x 128 of four 3-bit code-length-code lengths (0 = unused)
 __device__ __forceinline__ uint32_t kraft4(uint32_t f)
 {
@@ -416,7 +460,12 @@ __device__ bool stored_ok(const GlobalBits& G, const LdsBits& Lb, uint32_t bias,
         const uint32_t w = staged && lq + 8 + 32 <= lim ? Lb.peek(lq + 8) : G.peek(8 * (s + q + 1));
         return ((w & 0xffffu) ^ (w >> 16)) == 0xffffu;
     }
-    return type == 1 && L == 0;
+    // a fixed block after it: after an empty block, or (round 6) when its
+    // first symbols read as a real fixed block does (fixed_block_ok): a Beast
+    // peer's near-random payloads are runs of stored and fixed blocks
+    if (type != 1) return false;
+    if (L == 0) return true;
+    return staged && lq + 3 + FW * 9 + 32 <= lim ? fixed_block_ok(Lb, lq, lim) : fixed_block_ok(G, 8 * (s + q), 8 * (s + len));
 }
 
 // the most compressed bytes from one of this library's markers (or a stored
@@ -494,8 +543,9 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
             const uint32_t ri = region_map[gl];
             // (marked: bit 0 a sync marker, bit 1 a stored candidate within
             // MARK_SPAN + R of the payload's end -- a foreign encoder's payload
-            // that flushed once near its start is searched)
-            if ((marked[ri] | (BPMD_BP_MARK_END ? 0u : 2u)) == 3u || (gl - task_base[ri]) % dyn_stride != 0) {
+            // that flushed once near its start is searched; bit 2
+            // a stored block with data, which turns on the fixed-block search)
+            if (((marked[ri] & 3u) | (BPMD_BP_MARK_END ? 0u : 2u)) == 3u || (gl - task_base[ri]) % dyn_stride != 0) {
                 tasks[gl].kind = KIND_NONE;
             } else {
                 // a region inside the data of a stored block pass 1 found (one
@@ -533,6 +583,7 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
         const uint32_t i = (uint32_t)__builtin_amdgcn_readfirstlane((int)region_map[g]);
         const uint32_t m = order[i];
         const Stat st = stats[i];
+        const bool fixed_on = DYN && (marked[i] & 4u);   // pass 1's marks (an earlier launch)
         const uint32_t len = in_len[m];
         const uint32_t tb = task_base[i];
         const uint8_t* p = in + in_off[m];
@@ -636,14 +687,14 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
                 const bool near_end = (k + 1) * st.R + st.R + 2 * MARK_SPAN >= len;
                 if (k == 0) {
                     if (lane == 0) {
-                        if (best != 0xffffffffu && best_len == 0) atomicOr(&marked[i], 1u);
+                        if (best != 0xffffffffu) atomicOr(&marked[i], best_len == 0 ? 1u : 4u);
                         if (len <= 2 * MARK_SPAN || (best != 0xffffffffu && near_end)) atomicOr(&marked[i], 2u);
                     }
                     kind = KIND_START;
                 } else if (best != 0xffffffffu) {
                     bit = best;
                     kind = KIND_STORED;
-                    if (lane == 0) atomicOr(&marked[i], (best_len == 0 ? 1u : 0u) | (near_end ? 2u : 0u));
+                    if (lane == 0) atomicOr(&marked[i], (best_len == 0 ? 1u : 4u) | (near_end ? 2u : 0u));
                     BP_DIAG(if (lane == 0) atomicAdd(&g_bp_diag[5], 1ull));
                 } else if (!DYN) {
                     kind = KIND_PENDING;
@@ -667,6 +718,30 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
                             uint32_t cand = (uint32_t)mk;
                             if (first >= b1) cand = 0;
                             else if (b1 - first < 32) cand &= (1u << (b1 - first)) - 1u;
+                            // fixed-block starts after a fixed block (round 6): seven zero
+                            // bits (its end-of-block code), BFINAL 0, BTYPE 1 -- the bits
+                            // o - 7 .. o + 2 around offset o read 0000000 0 1 0.  Only in
+                            // payloads with a stored block of data (a Beast peer's
+                            // near-random runs): in a dynamic-coded text stream ~1 in 2 000
+                            // bits shows the pattern and ~0.6 % of those pass
+                            // fixed_block_ok, about one false start per 40 KiB payload
+                            // (each one sends the payload to the wave kernel)
+                            if (fixed_on) {
+                                const uint32_t wm = peek32(S, lb - 8);   // bits first - 8 ..
+                                const uint64_t x = ((uint64_t)w0 << 8 | (wm & 0xffu)) | ((uint64_t)w1 << 40);
+                                const uint64_t y = ~x;
+                                const uint64_t t1 = y & (y >> 1), t2 = t1 & (t1 >> 2), t3 = t2 & (t2 >> 4);   // 8 zeros
+                                uint32_t fm = (uint32_t)((t3 >> 1) & (x >> 9) & (y >> 10));
+                                if (first >= b1) fm = 0;
+                                else if (b1 - first < 32) fm &= (1u << (b1 - first)) - 1u;
+                                if (first < 8) fm &= ~0u << (8 - first);   // the zero bits lie in the payload
+                                while (fm) {
+                                    const uint32_t o = (uint32_t)__builtin_ctz(fm);
+                                    fm &= fm - 1;
+                                    const uint32_t at = atomicAdd(cnt, 1u);
+                                    if (at < LIST) list[at] = 0x80000000u | (first + o);
+                                }
+                            }
                             while (cand) {
                                 const uint32_t o = (uint32_t)__builtin_ctz(cand);
                                 cand &= cand - 1;
@@ -700,10 +775,13 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
                         if (lane == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         asm volatile("" ::: "memory");
                         for (uint32_t j0 = 0; j0 < nc; j0 += 64) {
+                            // (candidate bit << 1 | 1 for a fixed block: the min is the
+                            // first candidate, payload bits < 2^31)
                             uint32_t ok = 0xffffffffu;
                             if (j0 + lane < nc) {
-                                const uint32_t b = list[j0 + lane];
-                                if (dyn_header_ok(Lb, b + bias, lim)) ok = b;
+                                const uint32_t e = list[j0 + lane], b = e & 0x7fffffffu;
+                                if ((e >> 31) ? fixed_block_ok(Lb, b + bias, lim) : dyn_header_ok(Lb, b + bias, lim))
+                                    ok = (b << 1) | (e >> 31);
                             }
                             for (uint32_t d = 32; d >= 1; d >>= 1) {
                                 const uint32_t y = __shfl_xor(ok, d);
@@ -714,8 +792,8 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
                         __builtin_amdgcn_wave_barrier();
                     }
                     if (best != 0xffffffffu) {
-                        bit = best;
-                        kind = KIND_DYN;
+                        bit = best >> 1;
+                        kind = (best & 1u) ? KIND_FIXED : KIND_DYN;
                     }
                     BP_DIAG(if (lane == 0) atomicAdd(&g_bp_diag[10], __builtin_amdgcn_s_memtime() - t2));
                 }
@@ -782,7 +860,7 @@ bp_skim_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
     const SegTask t0 = tasks[g];
     if (t0.kind != KIND_START && t0.kind != KIND_STORED) continue;
     const uint32_t i = region_map[g];
-    if (marked[i] == 3u) continue;   // sync markers: pass 1 found the chunk starts
+    if ((marked[i] & 3u) == 3u) continue;   // sync markers: pass 1 found the chunk starts
     const Stat st = stats[i];
     const uint32_t tb = task_base[i];
     const uint32_t k0 = g - tb;

@@ -23,7 +23,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -40,6 +46,7 @@ extern "C" int bpmd_internal_deflate_bits_hist(const uint8_t* in, const uint64_t
                                                uint32_t* out_bits, const uint32_t* hist_len, int level,
                                                int window_bits, int strategy, const int* tune, hipStream_t stream,
                                                int64_t host_chunks);
+extern "C" int bpmd_internal_zstream_write_batch(const void* calls, uint32_t n, hipStream_t stream);
 
 struct bpmd_stream {
     bool is_deflate = true;
@@ -252,6 +259,9 @@ void reset_deflate(bpmd_stream* s)
     s->tuned = false;
 }
 
+// one flush's compression: through the micro-batcher when it is on (below)
+int run_flush(bpmd_stream* s, size_t out_cap, std::vector<uint8_t>& out, int32_t& status, uint32_t& bits);
+
 }  // namespace
 
 extern "C" int bpmd_deflate_stream_create(int level, int window_bits, int mem_level, int strategy,
@@ -316,7 +326,7 @@ extern "C" int bpmd_deflate_stream_write(bpmd_stream* s, bpmd_zparams* zs, int f
             int32_t st = 0;
             uint32_t nb = 0;
             const size_t cap = bpmd_deflate_upper_bound(s->in.size()) + 16;
-            int r = run_one(s, s->in.data(), s->in.size(), cap, out, st, nb);
+            int r = run_flush(s, cap, out, st, nb);
             if (r) return r;
             if (st != BPMD_OK) return BPMD_STREAM_ERROR;
             put_bitstring(s, out.data(), nb);
@@ -435,10 +445,9 @@ Head fresh_head(int window_bits)
     return h;
 }
 
-// the stream's device state, its result record and call buffers
-int ensure_zstate(bpmd_stream* s, size_t n_in, size_t cap)
+// the stream's device state (reset if a reset() is pending)
+int ensure_zhead(bpmd_stream* s)
 {
-    if (!s->hs && hipStreamCreateWithFlags(&s->hs, hipStreamNonBlocking) != hipSuccess) return BPMD_R_HIP_ERROR;
     if (!s->zst) {
         if (hipMalloc(&s->zst, sizeof(State) + sizeof(Result)) != hipSuccess) {
             s->zst = nullptr;
@@ -451,6 +460,13 @@ int ensure_zstate(bpmd_stream* s, size_t n_in, size_t cap)
         if (hipMemcpy(s->zst, &h, sizeof h, hipMemcpyHostToDevice) != hipSuccess) return BPMD_R_HIP_ERROR;
         s->zreset = false;
     }
+    return BPMD_R_OK;
+}
+
+// ... and the single-call path's stream and input / output buffers
+int ensure_zbuf(bpmd_stream* s, size_t n_in, size_t cap)
+{
+    if (!s->hs && hipStreamCreateWithFlags(&s->hs, hipStreamNonBlocking) != hipSuccess) return BPMD_R_HIP_ERROR;
     // input and output buffers, with slack for the 16-byte input staging loads
     if (n_in + 64 > s->din_cap) {
         if (s->din) (void)hipFree(s->din);
@@ -471,7 +487,426 @@ int ensure_zstate(bpmd_stream* s, size_t n_in, size_t cap)
     return BPMD_R_OK;
 }
 
+// one write() on the stream's own HIP stream: the input is uploaded, the
+// kernel runs, and the result record and output come back (the output
+// lands in the caller's buffer whether or not done() publishes it)
+int inflate_one(bpmd_stream* s, const uint8_t* in, size_t n, uint8_t* out, size_t cap, int flush, Result& res)
+{
+    int r = ensure_zbuf(s, n, cap);
+    if (r) return r;
+    const hipStream_t hs = s->hs;
+    // the result record and the output share one device block, so one D2H
+    // brings both back when the output is at most `spec` bytes (pinned
+    // staging for both directions: each copy is one DMA)
+    constexpr size_t RES_AT = 64;
+    const size_t spec = std::min<size_t>(cap, 16384);
+    uint8_t* h = pinned(s, std::max(n, RES_AT + spec) + 64);
+    if (!h) return BPMD_R_HIP_ERROR;
+    if (n) std::memcpy(h, in, n);
+    bool ok = (n == 0 || hipMemcpyAsync(s->din, h, n, hipMemcpyHostToDevice, hs) == hipSuccess) &&
+              bpmd_internal_zstream_write(s->zst, s->din, n, s->dout + RES_AT, cap, flush, s->dout, hs) == 0 &&
+              hipMemcpyAsync(h, s->dout, RES_AT + spec, hipMemcpyDeviceToHost, hs) == hipSuccess &&
+              hipStreamSynchronize(hs) == hipSuccess;
+    if (ok) std::memcpy(&res, h, sizeof res);
+    ok = ok && res.out_used <= cap;
+    if (ok && res.out_used) {
+        std::memcpy(out, h + RES_AT, std::min<size_t>(res.out_used, spec));
+        if (res.out_used > spec)
+            ok = hipMemcpy(out + spec, s->dout + RES_AT + spec, res.out_used - spec, hipMemcpyDeviceToHost) ==
+                 hipSuccess;
+    }
+    if (!ok) {
+        // the pinned staging buffer may still be a DMA's source or target
+        (void)hipStreamSynchronize(hs);
+        return BPMD_R_HIP_ERROR;   // the device state is unchanged only if the kernel never ran
+    }
+    return BPMD_R_OK;
+}
+
 }  // namespace
+
+// ------------------------------------------------------------ micro-batcher
+// write() calls of different streams made at the same time
+// -- a server's connections, each reading and writing on its own thread or
+// strand (impl_base.hpp:85-190 inflate / deflate calls, write.hpp:463-545)
+// -- run as one launch.  A call queues itself; if no batch is running it
+// becomes the leader: it takes up to max_calls queued calls (one per stream),
+// runs them together and wakes their callers.  Calls that arrive while a
+// batch runs form the next one (a group commit: no added latency when a
+// stream is alone -- a batch of one takes the single-call path), and
+// max_delay_us > 0 lets a leader wait that long for more.  Every call's
+// result is its single-call result: the inflate launch runs the same
+// per-stream state machine for each stream (one workgroup per call,
+// pmd_zstream.hip), the deflate launch the same per-message kernels, whose
+// bytes do not depend on the batch's other messages.
+namespace {
+
+struct Job {
+    bpmd_stream* s = nullptr;
+    // inflate: the caller's input and output room
+    const uint8_t* in = nullptr;
+    size_t n = 0;
+    uint8_t* out = nullptr;
+    size_t cap = 0;
+    int flush = 0;
+    Result res{};
+    // deflate: the stream's buffered input (s->in) and where its output goes
+    size_t out_cap = 0;
+    std::vector<uint8_t>* dout = nullptr;
+    int32_t status = 0;
+    uint32_t bits = 0;
+    int rc = 0;
+    bool done = false;
+};
+
+// a leader's device block, its pinned mirror and the HIP stream they use
+struct Arena {
+    hipStream_t hs = nullptr;
+    uint8_t* d = nullptr;
+    uint8_t* h = nullptr;
+    size_t cap = 0;
+    bool reserve(size_t need)
+    {
+        if (!hs && hipStreamCreateWithFlags(&hs, hipStreamNonBlocking) != hipSuccess) {
+            hs = nullptr;
+            return false;
+        }
+        if (need <= cap) return true;
+        if (d) (void)hipFree(d);
+        if (h) (void)hipHostFree(h);
+        d = h = nullptr;
+        cap = 0;
+        const size_t c = std::max<size_t>(need + need / 2, 1 << 20);
+        if (hipMalloc((void**)&d, c) != hipSuccess) {
+            d = nullptr;
+            return false;
+        }
+        if (hipHostMalloc((void**)&h, c, hipHostMallocDefault) != hipSuccess) {
+            (void)hipFree(d);
+            d = h = nullptr;
+            return false;
+        }
+        cap = c;
+        return true;
+    }
+};
+
+// settings: max_calls < 2 is off
+std::atomic<int> g_bmax{-1}, g_bdelay{-1};
+// [0] inflate calls, [1] inflate launches, [2] deflate flushes, [3] deflate launches
+std::atomic<unsigned long long> g_bstat[4];
+
+int batch_max()
+{
+    int m = g_bmax.load();
+    if (m < 0) {
+        const char* e = getenv("BPMD_STREAM_BATCH");
+        m = e ? std::max(0, std::min(atoi(e), 4096)) : 256;
+        const char* d = getenv("BPMD_STREAM_BATCH_DELAY_US");
+        g_bdelay.store(d ? std::max(0, atoi(d)) : 0);
+        g_bmax.store(m);
+    }
+    return m;
+}
+
+class Coalescer {
+  public:
+    template <class Exec>
+    void run(Job* j, int max_calls, Exec&& exec)
+    {
+        std::unique_lock<std::mutex> lk(mu_);
+        q_.push_back(j);
+        if (busy_) arrive_.notify_one();
+        while (!j->done) {
+            if (busy_) {
+                done_.wait(lk);
+                continue;
+            }
+            busy_ = true;
+            const int delay = g_bdelay.load();
+            if (delay > 0 && q_.size() < (size_t)max_calls)
+                arrive_.wait_for(lk, std::chrono::microseconds(delay), [&] { return q_.size() >= (size_t)max_calls; });
+            // in arrival order, one call per stream (a stream's calls are
+            // its owner's sequence: a second one waits for the next batch)
+            std::vector<Job*> take;
+            for (auto it = q_.begin(); it != q_.end() && take.size() < (size_t)max_calls;) {
+                bool dup = false;
+                for (const Job* t : take) dup = dup || t->s == (*it)->s;
+                if (dup) {
+                    ++it;
+                    continue;
+                }
+                take.push_back(*it);
+                it = q_.erase(it);
+            }
+            lk.unlock();
+            exec(arena_, take);
+            lk.lock();
+            for (Job* t : take) t->done = true;
+            busy_ = false;
+            done_.notify_all();
+        }
+    }
+
+  private:
+    std::mutex mu_;
+    std::condition_variable done_, arrive_;
+    std::deque<Job*> q_;
+    bool busy_ = false;
+    Arena arena_;
+};
+
+// process-lifetime objects (never destroyed: HIP may be torn down first)
+Coalescer& inflate_coalescer()
+{
+    static Coalescer* c = new Coalescer();
+    return *c;
+}
+Coalescer& deflate_coalescer()
+{
+    static Coalescer* c = new Coalescer();
+    return *c;
+}
+
+constexpr size_t up256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+void fail_all(std::vector<Job*>& jobs, hipStream_t hs)
+{
+    if (hs) (void)hipStreamSynchronize(hs);   // no DMA may still use the pinned mirror
+    for (Job* j : jobs) j->rc = BPMD_R_HIP_ERROR;
+}
+
+// k >= 2 inflate write() calls as one launch.  Block: [ZCall k][inputs]
+// [Result k][outputs]; one H2D of calls + inputs, the launch, one D2H of the
+// results and outputs (of the results alone, then each call's used output,
+// when the output room is over 4 MiB).
+void inflate_batch(Arena& A, std::vector<Job*>& jobs)
+{
+    using bpmd::zst::ZCall;
+    const uint32_t k = (uint32_t)jobs.size();
+    std::vector<size_t> ioff(k), ooff(k);
+    size_t o = up256(sizeof(ZCall) * k);
+    for (uint32_t i = 0; i < k; ++i) {
+        ioff[i] = o;
+        o = up256(o + jobs[i]->n + 64);   // + the staging loads' slack
+    }
+    const size_t res_at = o;
+    o = up256(res_at + 64ull * k);
+    for (uint32_t i = 0; i < k; ++i) {
+        ooff[i] = o;
+        o = up256(o + jobs[i]->cap);
+    }
+    const size_t total = o;
+    if (!A.reserve(total)) return fail_all(jobs, A.hs);
+    ZCall* zc = (ZCall*)A.h;
+    for (uint32_t i = 0; i < k; ++i) {
+        const Job* j = jobs[i];
+        if (j->n) std::memcpy(A.h + ioff[i], j->in, j->n);
+        ZCall c{};
+        c.st = j->s->zst;
+        c.in = A.d + ioff[i];
+        c.n_in = j->n;
+        c.out = A.d + ooff[i];
+        c.cap = j->cap;
+        c.res = A.d + res_at + 64ull * i;
+        c.flush = j->flush;
+        zc[i] = c;
+    }
+    const bool whole = total - res_at <= (4u << 20);
+    bool ok = hipMemcpyAsync(A.d, A.h, res_at, hipMemcpyHostToDevice, A.hs) == hipSuccess &&
+              bpmd_internal_zstream_write_batch(A.d, k, A.hs) == 0 &&
+              hipMemcpyAsync(A.h + res_at, A.d + res_at, (whole ? total : res_at + 64ull * k) - res_at,
+                             hipMemcpyDeviceToHost, A.hs) == hipSuccess &&
+              hipStreamSynchronize(A.hs) == hipSuccess;
+    if (!ok) return fail_all(jobs, A.hs);
+    for (uint32_t i = 0; i < k && ok; ++i) {
+        Job* j = jobs[i];
+        std::memcpy(&j->res, A.h + res_at + 64ull * i, sizeof(Result));
+        ok = j->res.out_used <= j->cap;
+        if (ok && !whole && j->res.out_used)
+            ok = hipMemcpyAsync(A.h + ooff[i], A.d + ooff[i], j->res.out_used, hipMemcpyDeviceToHost, A.hs) ==
+                 hipSuccess;
+    }
+    if (ok && !whole) ok = hipStreamSynchronize(A.hs) == hipSuccess;
+    if (!ok) return fail_all(jobs, A.hs);
+    for (uint32_t i = 0; i < k; ++i) {
+        Job* j = jobs[i];
+        if (j->res.out_used) std::memcpy(j->out, A.h + ooff[i], j->res.out_used);
+        j->rc = BPMD_R_OK;
+    }
+}
+
+void inflate_exec(Arena& A, std::vector<Job*>& jobs)
+{
+    g_bstat[1].fetch_add(1);
+    if (jobs.size() == 1) {
+        Job* j = jobs[0];
+        j->rc = inflate_one(j->s, j->in, j->n, j->out, j->cap, j->flush, j->res);
+        return;
+    }
+    inflate_batch(A, jobs);
+}
+
+// deflate flushes with the same parameters (level, windowBits, strategy,
+// tune values, history or not) as one call of the deflater.  Block:
+// [SoA meta][outputs][history + input, per flush]; H2D of meta and inputs,
+// the kernels (the chunk count is known here: nothing is read back), one D2H
+// of meta + outputs (meta, then each flush's output, past 4 MiB of room).
+void deflate_group(Arena& A, std::vector<Job*>& jobs)
+{
+    const uint32_t k = (uint32_t)jobs.size();
+    const bpmd_stream* s0 = jobs[0]->s;
+    const bool hist = !s0->hist.empty();
+    const size_t m_in_off = 0, m_out_off = 8ull * k, m_in_len = 16ull * k, m_out_cap = 20ull * k,
+                 m_hist = 24ull * k, m_out_len = 28ull * k, m_bits = 32ull * k, m_status = 36ull * k;
+    const size_t out_at = up256(40ull * k);
+    std::vector<uint64_t> oo(k), io(k);
+    size_t o = 0;
+    for (uint32_t i = 0; i < k; ++i) {
+        oo[i] = o;
+        o = up256(o + jobs[i]->out_cap);
+    }
+    const size_t in_at = out_at + o;
+    size_t ib = 0;
+    int64_t chunks = 0;
+    for (uint32_t i = 0; i < k; ++i) {
+        const bpmd_stream* s = jobs[i]->s;
+        const size_t hn = s->hist.size(), n = s->in.size();
+        if (n + hn > 0xFFFFFFFFu || jobs[i]->out_cap > 0xFFFFFFFFu) {
+            for (Job* j : jobs) j->rc = BPMD_R_INVALID_ARGUMENT;
+            return;
+        }
+        io[i] = ib;
+        ib = up256(ib + hn + n);
+        // run_one's count (pmd_deflate.hip chunk_count)
+        chunks += hn ? (int64_t)((n + 4095) / 4096) : (n > 4096 ? (int64_t)((n + 4095) / 4096) : 0);
+    }
+    const size_t total = in_at + ib + 16;
+    if (!A.reserve(total)) return fail_all(jobs, A.hs);
+    uint8_t* h = A.h;
+    std::memset(h, 0, out_at);
+    for (uint32_t i = 0; i < k; ++i) {
+        const bpmd_stream* s = jobs[i]->s;
+        const size_t hn = s->hist.size(), n = s->in.size();
+        ((uint64_t*)(h + m_in_off))[i] = io[i] + hn;
+        ((uint64_t*)(h + m_out_off))[i] = oo[i];
+        ((uint32_t*)(h + m_in_len))[i] = (uint32_t)n;
+        ((uint32_t*)(h + m_out_cap))[i] = (uint32_t)jobs[i]->out_cap;
+        ((uint32_t*)(h + m_hist))[i] = (uint32_t)hn;
+        if (hn) std::memcpy(h + in_at + io[i], s->hist.data(), hn);
+        if (n) std::memcpy(h + in_at + io[i] + hn, s->in.data(), n);
+    }
+    uint8_t* d = A.d;
+    const bool whole = in_at <= (4u << 20);
+    bool ok = hipMemcpyAsync(d, h, out_at, hipMemcpyHostToDevice, A.hs) == hipSuccess &&
+              (ib == 0 || hipMemcpyAsync(d + in_at, h + in_at, ib, hipMemcpyHostToDevice, A.hs) == hipSuccess) &&
+              bpmd_internal_deflate_bits_hist(d + in_at, (const uint64_t*)(d + m_in_off),
+                                              (const uint32_t*)(d + m_in_len), k, d + out_at,
+                                              (const uint64_t*)(d + m_out_off), (const uint32_t*)(d + m_out_cap),
+                                              (uint32_t*)(d + m_out_len), (int32_t*)(d + m_status),
+                                              (uint32_t*)(d + m_bits), hist ? (const uint32_t*)(d + m_hist) : nullptr,
+                                              s0->level, s0->wbits, s0->strategy, s0->tuned ? s0->tune4 : nullptr,
+                                              A.hs, chunks) == 0 &&
+              hipMemcpyAsync(h, d, whole ? in_at : out_at, hipMemcpyDeviceToHost, A.hs) == hipSuccess &&
+              hipStreamSynchronize(A.hs) == hipSuccess;
+    if (!ok) return fail_all(jobs, A.hs);
+    for (uint32_t i = 0; i < k && ok; ++i) {
+        const uint32_t len = ((const uint32_t*)(h + m_out_len))[i];
+        ok = len <= jobs[i]->out_cap;
+        if (ok && !whole && len)
+            ok = hipMemcpyAsync(h + out_at + oo[i], d + out_at + oo[i], len, hipMemcpyDeviceToHost, A.hs) ==
+                 hipSuccess;
+    }
+    if (ok && !whole) ok = hipStreamSynchronize(A.hs) == hipSuccess;
+    if (!ok) return fail_all(jobs, A.hs);
+    for (uint32_t i = 0; i < k; ++i) {
+        Job* j = jobs[i];
+        const uint32_t len = ((const uint32_t*)(h + m_out_len))[i];
+        j->dout->assign(h + out_at + oo[i], h + out_at + oo[i] + len);
+        j->status = ((const int32_t*)(h + m_status))[i];
+        j->bits = ((const uint32_t*)(h + m_bits))[i];
+        j->rc = BPMD_R_OK;
+    }
+}
+
+bool same_params(const bpmd_stream* a, const bpmd_stream* b)
+{
+    return a->level == b->level && a->wbits == b->wbits && a->strategy == b->strategy && a->tuned == b->tuned &&
+           (!a->tuned || std::memcmp(a->tune4, b->tune4, sizeof a->tune4) == 0) &&
+           a->hist.empty() == b->hist.empty();
+}
+
+void deflate_exec(Arena& A, std::vector<Job*>& jobs)
+{
+    std::vector<bool> used(jobs.size(), false);
+    for (size_t i = 0; i < jobs.size(); ++i) {
+        if (used[i]) continue;
+        std::vector<Job*> g{jobs[i]};
+        for (size_t j = i + 1; j < jobs.size(); ++j)
+            if (!used[j] && same_params(jobs[i]->s, jobs[j]->s)) {
+                used[j] = true;
+                g.push_back(jobs[j]);
+            }
+        g_bstat[3].fetch_add(1);
+        if (g.size() == 1) {
+            Job* j = g[0];
+            j->rc = run_one(j->s, j->s->in.data(), j->s->in.size(), j->out_cap, *j->dout, j->status, j->bits);
+        } else {
+            deflate_group(A, g);
+        }
+    }
+}
+
+// the inflate write()'s call, batched or not
+int inflate_call(bpmd_stream* s, const uint8_t* in, size_t n, uint8_t* out, size_t cap, int flush, Result& res)
+{
+    const int mx = batch_max();
+    if (mx < 2) return inflate_one(s, in, n, out, cap, flush, res);
+    g_bstat[0].fetch_add(1);
+    Job j;
+    j.s = s;
+    j.in = in;
+    j.n = n;
+    j.out = out;
+    j.cap = cap;
+    j.flush = flush;
+    inflate_coalescer().run(&j, mx, inflate_exec);
+    res = j.res;
+    return j.rc;
+}
+
+int run_flush(bpmd_stream* s, size_t out_cap, std::vector<uint8_t>& out, int32_t& status, uint32_t& bits)
+{
+    const int mx = batch_max();
+    if (mx < 2) return run_one(s, s->in.data(), s->in.size(), out_cap, out, status, bits);
+    g_bstat[2].fetch_add(1);
+    Job j;
+    j.s = s;
+    j.out_cap = out_cap;
+    j.dout = &out;
+    deflate_coalescer().run(&j, mx, deflate_exec);
+    status = j.status;
+    bits = j.bits;
+    return j.rc;
+}
+
+}  // namespace
+
+extern "C" int bpmd_stream_batching(int max_calls, int max_delay_us)
+{
+    if (max_calls < 0 || max_calls > 4096 || max_delay_us < 0) return BPMD_R_INVALID_ARGUMENT;
+    (void)batch_max();   // the environment's defaults read first, then replaced
+    g_bdelay.store(max_delay_us);
+    g_bmax.store(max_calls);
+    return BPMD_R_OK;
+}
+
+extern "C" int bpmd_stream_batch_stats(unsigned long long* out, int reset)
+{
+    if (!out) return BPMD_R_INVALID_ARGUMENT;
+    for (int i = 0; i < 4; ++i) out[i] = reset ? g_bstat[i].exchange(0) : g_bstat[i].load();
+    return BPMD_R_OK;
+}
 
 extern "C" int bpmd_inflate_stream_reset(bpmd_stream* s, int window_bits)
 {
@@ -503,35 +938,9 @@ extern "C" int bpmd_inflate_stream_write(bpmd_stream* s, bpmd_zparams* zs, int f
     // reference's "avail_out >= 258" fast-path test unchanged.
     const size_t bound = 1040 * n + 8192;
     const size_t cap = std::min<size_t>(zs->avail_out, bound);
-    if ((r = ensure_zstate(s, n, cap)) != 0) return r;
-    const hipStream_t hs = s->hs;
+    if ((r = ensure_zhead(s)) != 0) return r;
     Result res{};
-    // the result record and the output share one device block, so one D2H
-    // brings both back when the output is at most `spec` bytes (pinned
-    // staging for both directions: each copy is one DMA)
-    constexpr size_t RES_AT = 64;
-    const size_t spec = std::min<size_t>(cap, 16384);
-    uint8_t* h = pinned(s, std::max(n, RES_AT + spec) + 64);
-    if (!h) return BPMD_R_HIP_ERROR;
-    if (n) std::memcpy(h, zs->next_in, n);
-    bool ok = (n == 0 || hipMemcpyAsync(s->din, h, n, hipMemcpyHostToDevice, hs) == hipSuccess) &&
-              bpmd_internal_zstream_write(s->zst, s->din, n, s->dout + RES_AT, cap, flush, s->dout, hs) == 0 &&
-              hipMemcpyAsync(h, s->dout, RES_AT + spec, hipMemcpyDeviceToHost, hs) == hipSuccess &&
-              hipStreamSynchronize(hs) == hipSuccess;
-    if (ok) std::memcpy(&res, h, sizeof res);
-    // the bytes are in the caller's buffer whether or not done() publishes them
-    ok = ok && res.out_used <= cap;
-    if (ok && res.out_used) {
-        std::memcpy(zs->next_out, h + RES_AT, std::min<size_t>(res.out_used, spec));
-        if (res.out_used > spec)
-            ok = hipMemcpy((uint8_t*)zs->next_out + spec, s->dout + RES_AT + spec, res.out_used - spec,
-                           hipMemcpyDeviceToHost) == hipSuccess;
-    }
-    if (!ok) {
-        // the pinned staging buffer may still be a DMA's source or target
-        (void)hipStreamSynchronize(hs);
-        return BPMD_R_HIP_ERROR;   // the device state is unchanged only if the kernel never ran
-    }
+    if ((r = inflate_call(s, (const uint8_t*)zs->next_in, n, (uint8_t*)zs->next_out, cap, flush, res)) != 0) return r;
     if (res.published) {
         zs->next_in = (const uint8_t*)zs->next_in + res.in_used;
         zs->avail_in -= res.in_used;

@@ -1343,6 +1343,16 @@ zstream_write_kernel(State* __restrict__ st, const uint8_t* __restrict__ in, uin
 #endif
     zstream_run(L, st, in, n_in, out, cap, flush, res, par & 9);
 }
+
+// the micro-batcher's launch (pmd_stream.hip): one write() of a different
+// stream per workgroup, each exactly the call zstream_write_kernel makes
+__global__ void __launch_bounds__(WAVE)
+zstream_write_batch_kernel(const ZCall* __restrict__ calls, int par)
+{
+    __shared__ Lds L;
+    const ZCall c = calls[blockIdx.x];
+    zstream_run(L, (State*)c.st, c.in, c.n_in, c.out, c.cap, c.flush, (Result*)c.res, par & 9);
+}
 #endif
 
 }  // namespace zst
@@ -1383,6 +1393,23 @@ extern "C" int bpmd_internal_zstream_write(void* st, const uint8_t* in, uint64_t
 #endif
     hipLaunchKernelGGL(zstream_write_kernel, dim3(1), dim3(bpmd::WAVE), 0, stream, (State*)st, in, n_in, out, cap,
                        flush, (Result*)res, par);
+    return (int)hipGetLastError();
+}
+
+// n write() calls of n different streams in one launch (calls: device array
+// of bpmd::zst::ZCall)
+extern "C" int bpmd_internal_zstream_write_batch(const void* calls, uint32_t n, hipStream_t stream)
+{
+    using namespace bpmd::zst;
+    if (n == 0) return 0;
+    static const int env_par = [] {
+        const char* e = getenv("BPMD_ZSTREAM_PAR");
+        const char* hp = getenv("BPMD_ZSTREAM_HPAR");
+        return (e ? (atoi(e) ? 1 : 0) : 1) | (hp && hp[0] == '0' ? 8 : 0);
+    }();
+    const int o = g_zst_par.load();
+    const int par = o < 0 ? env_par : o;
+    hipLaunchKernelGGL(zstream_write_batch_kernel, dim3(n), dim3(bpmd::WAVE), 0, stream, (const ZCall*)calls, par);
     return (int)hipGetLastError();
 }
 

@@ -50,5 +50,19 @@ struct Result {
     int32_t pad;
 };
 
+// one write() of a batched launch (pmd_stream.hip's micro-batcher): the
+// stream's device State, its input, output room and Result record
+struct ZCall {
+    void* st;
+    const uint8_t* in;
+    uint64_t n_in;
+    uint8_t* out;
+    uint64_t cap;
+    void* res;
+    int32_t flush;
+    int32_t pad[3];
+};
+static_assert(sizeof(ZCall) == 64, "call record");
+
 }  // namespace zst
 }  // namespace bpmd

@@ -443,6 +443,22 @@ int bpmd_inflate_stream_write(bpmd_stream* s, bpmd_zparams* zs, int flush);
 int bpmd_inflate_stream_footprint(const bpmd_stream* s, size_t* host_bytes, size_t* device_bytes);
 void bpmd_stream_destroy(bpmd_stream* s);
 
+/* The micro-batcher behind the two write() calls above (no reference
+ * counterpart; SURVEY §8(f) N2, for the call sites impl_base.hpp:85-190 and
+ * write.hpp:463-545): calls of different streams made at the same time run
+ * as one launch, each with exactly its single-call result (status, output
+ * bytes, every z_params field).  A call that finds no batch running takes
+ * up to max_calls queued calls (one per stream) and runs them; calls that
+ * arrive meanwhile form the next batch, so a lone stream waits for nothing
+ * (its batch of one is the single-call path).  max_delay_us > 0: a batch's
+ * first call also waits up to that long for more.  max_calls < 2 turns it
+ * off.  Default: 256 calls, no delay (environment: BPMD_STREAM_BATCH,
+ * BPMD_STREAM_BATCH_DELAY_US). */
+int bpmd_stream_batching(int max_calls, int max_delay_us);
+/* out[0] inflate write() calls through the batcher, out[1] their launches,
+ * out[2] deflate flushes, out[3] their deflater calls; reset != 0 zeroes them. */
+int bpmd_stream_batch_stats(unsigned long long* out, int reset);
+
 #ifdef __cplusplus
 }
 #endif

@@ -162,6 +162,7 @@ static std::vector<uint8_t> encode(const uint8_t* msg, unsigned n, const Params&
         const uint8_t* w = msg + wb;
         unsigned wn = cend - wb, a0 = base - wb;
         std::vector<Tok> toks;
+        bool chunk_incomp = false;
         if (L.parser != P_STORED) {
             prev.assign(wn, -1);
             std::fill(head.begin(), head.end(), -1);
@@ -179,6 +180,7 @@ static std::vector<uint8_t> encode(const uint8_t* msg, unsigned n, const Params&
                     hits += prev[q] >= 0 && memcmp(w + prev[q], w + q, 4) == 0;
                 no_parse = incompressible(hits, wn - a0);
             }
+            chunk_incomp = no_parse;
             unsigned len = wn - a0;
             unsigned seg = (len + P.lanes - 1) / P.lanes;
             const unsigned min_seg = a0 ? 32u : (unsigned)P.min_seg;   // (pmd_deflate.hip: history keeps 32)
@@ -253,7 +255,10 @@ static std::vector<uint8_t> encode(const uint8_t* msg, unsigned n, const Params&
         unsigned clen = cend - base;
         uint64_t opt_b = (dyn_bits + 7) >> 3, fix_b = (fix_bits + 7) >> 3;
         if (P.strategy == 4) opt_b = fix_b + 1;
-        if (L.parser == P_STORED || (uint64_t)clen + 4 <= (opt_b < fix_b ? opt_b : fix_b)) {
+        // an incompressible chunk of a multi-chunk message: stored outright
+        // (lz_core.h INCOMP_STORED)
+        if (L.parser == P_STORED || (INCOMP_STORED && chunk_incomp && n > (unsigned)P.chunk) ||
+            (uint64_t)clen + 4 <= (opt_b < fix_b ? opt_b : fix_b)) {
             if (base == (unsigned)P.chunk) marker(base);   // chunk 1 carries a marker whatever its kind
             bw.put(0, 3);
             bw.align();

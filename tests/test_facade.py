@@ -36,7 +36,7 @@ def _build(name):
     return out
 
 
-@pytest.mark.parametrize("name", ["facade_roundtrip", "ws_echo", "write_threshold"])
+@pytest.mark.parametrize("name", ["facade_roundtrip", "ws_echo", "write_threshold", "batch_streams"])
 def test_facade_compiles_and_links(name):
     assert os.path.exists(_build(name))
 
@@ -52,20 +52,21 @@ def test_impl_base_codec_uses_compile():
     assert r.returncode == 0, r.stderr
 
 
-def _build_cpu_echo():
-    """ws_echo.cpp linked against tests/cpp/oracle_backend.c (Beast's zlib
-    restated, CPU) instead of libbeast_pmd.so: the same C1 harness, timed
-    the same way, with the reference's CPU codec (test infrastructure)."""
+def _build_cpu_echo(name="ws_echo"):
+    """ws_echo.cpp (or another harness) linked against
+    tests/cpp/oracle_backend.c (Beast's zlib restated, CPU) instead of
+    libbeast_pmd.so: the same harness, timed the same way, with the
+    reference's CPU codec (test infrastructure)."""
     os.makedirs(BUILD, exist_ok=True)
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "liboracle.so"], check=True)
     odir = os.path.join(ROOT, "oracle")
     lib = os.path.join(BUILD, "libbpmd_oracle_backend.so")
-    out = os.path.join(BUILD, "ws_echo_cpu")
+    out = os.path.join(BUILD, name + "_cpu")
     subprocess.run(["gcc", "-O2", "-fPIC", "-shared", "-o", lib, os.path.join(CPP, "oracle_backend.c"),
                     "-L", odir, "-loracle", f"-Wl,-rpath,{odir}"], check=True)
-    subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
-                    os.path.join(CPP, "ws_echo.cpp"), "-o", out, "-L", BUILD, "-lbpmd_oracle_backend",
-                    f"-Wl,-rpath,{BUILD}", "-lpthread"], check=True)
+    subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", "-Werror", "-DBPMD_CPU_BACKEND", "-I",
+                    os.path.join(ROOT, "include"), os.path.join(CPP, name + ".cpp"), "-o", out, "-L", BUILD,
+                    "-lbpmd_oracle_backend", f"-Wl,-rpath,{BUILD}", "-lpthread"], check=True)
     return out
 
 
@@ -133,3 +134,45 @@ def test_msg_size_threshold_on_gpu():
     fewer bytes than its size."""
     r = subprocess.run([_build("write_threshold"), "gpu"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "issue1666" in r.stdout, r.stdout + r.stderr
+
+
+def _rate(out, key):
+    import re
+    m = re.search(key + r".*?([0-9.]+) MB/s", out)
+    return float(m.group(1))
+
+
+def test_batch_streams_cpu_codec():
+    """The N2 harness on Beast's CPU codec: 64 threads, each a connection's
+    never-reset codec pair, round-trip their messages exactly."""
+    r = subprocess.run([_build_cpu_echo("batch_streams"), "64", "8", "1024"], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "cpu codec: 64 threads" in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("size", [1024, 16384])
+def test_stream_batcher_64_threads_on_gpu(size):
+    """N2: 64 threads, each running impl_base's deflate
+    and read-path inflate sequences on its own drop-in streams
+    (tests/cpp/batch_streams.cpp), first with the micro-batcher off, then on
+    (pmd_stream.hip).  Every message round-trips, every batched payload byte
+    equals the unbatched one, and the batched run makes fewer launches than
+    write() calls, inflate and deflate both.  Rates of both runs and of
+    Beast's CPU codec on the same 64 threads are printed."""
+    import re
+    r = subprocess.run([_build("batch_streams"), "64", "24", str(size)], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "payloads equal: 64 x 24" in r.stdout, r.stdout
+    m = re.search(r"inflate calls (\d+) launches (\d+); deflate flushes (\d+) launches (\d+)", r.stdout)
+    ic, il, dc, dl = map(int, m.groups())
+    assert ic >= 64 * 24 * 2 and dc == 64 * 24, r.stdout
+    assert il < ic and dl < dc, r.stdout
+    c = subprocess.run([_build_cpu_echo("batch_streams"), "64", "24", str(size)], capture_output=True, text=True,
+                       timeout=300)
+    assert c.returncode == 0, c.stdout + c.stderr
+    print(f"N2 {size} B: GPU unbatched {_rate(r.stdout, 'unbatched'):.1f} MB/s, batched "
+          f"{_rate(r.stdout, 'batched'):.1f} MB/s ({ic} inflate calls in {il} launches, {dc} deflate flushes in "
+          f"{dl}); Beast CPU codec {_rate(c.stdout, 'cpu codec'):.1f} MB/s, 64 threads")
