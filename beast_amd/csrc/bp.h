@@ -23,6 +23,9 @@ namespace bp {
 constexpr int32_t SEG_HANDOFF = 100;   // stopped at the next candidate's header
 constexpr int32_t SEG_FULL = 101;      // the symbol slot is full
 constexpr int32_t SEG_SKIP = 102;      // no candidate in this region
+// a stored block that ends where the next candidate starts: nothing decoded,
+// the resolve copies its nsym bytes from the payload (after its LEN / NLEN)
+constexpr int32_t SEG_DIRECT = 103;
 
 constexpr uint32_t KIND_START = 0;    // the payload's first bit
 constexpr uint32_t KIND_DYN = 1;      // a validated dynamic-block header (bit = its first bit)

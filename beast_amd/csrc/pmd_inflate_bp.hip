@@ -359,10 +359,25 @@ __device__ bool dyn_header_ok(const Bits& B, uint32_t b, uint32_t lim)
 // codes 257-279 and 8-bit 280-285), the near-random data a Beast peer codes
 // in fixed blocks as 0-5 % (C5: tr_flush_block picks fixed for it,
 // deflate_stream.ipp:1425-1518): the test tells a real block start from the
-// ~8 random offsets per KiB that show a fixed header after seven zero bits
-// (a fixed block's end-of-block code).  A block it rejects -- a fixed block
-// of text with many matches, say -- is only not a segment start.
-constexpr uint32_t FW = 48, FMAX = 4;
+// ~4 random offsets per KiB that show a fixed header after seven zero bits
+// (a fixed block's end-of-block code).  Random bits pass about 1 in 10^4
+// (96 symbols, at most 6 lengths; 48 and 4 let ~0.3 % through, about one
+// false start per Beast C5 payload: a segment before two of them gets a slot
+// sized short, and 21-37 % of the payloads fell back to the wave kernel,
+// profiles/r06l_beast_shard.log).  A block it rejects -- a fixed block of
+// text with many matches, say -- is only not a segment start.  (FW * 9 bits
+// fit in STAGE_EXTRA.)
+#ifndef BPMD_BP_FIXED
+// bit 0: a stored block followed by a fixed block that passes fixed_block_ok
+// is a candidate (round 5: only an empty one); bit 1: pass 2 also searches
+// fixed-block starts after a fixed block's end-of-block code.  Inside a fixed
+// block of literals that pattern shows ~4 times per KiB, and decoding from
+// there resynchronises with the block's own codes within a few symbols, so
+// such a false start passes fixed_block_ok: the pass-2 search is off
+// (profiles/r06l_beast_shard.log: 21-37 % of C5's Beast payloads fell back)
+#define BPMD_BP_FIXED 1
+#endif
+constexpr uint32_t FW = 96, FMAX = 6;
 template <class Bits>
 __device__ bool fixed_block_ok(const Bits& B, uint32_t b, uint32_t lim)
 {
@@ -465,6 +480,7 @@ __device__ bool stored_ok(const GlobalBits& G, const LdsBits& Lb, uint32_t bias,
     // peer's near-random payloads are runs of stored and fixed blocks
     if (type != 1) return false;
     if (L == 0) return true;
+    if (!(BPMD_BP_FIXED & 1)) return false;
     return staged && lq + 3 + FW * 9 + 32 <= lim ? fixed_block_ok(Lb, lq, lim) : fixed_block_ok(G, 8 * (s + q), 8 * (s + len));
 }
 
@@ -583,7 +599,7 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
         const uint32_t i = (uint32_t)__builtin_amdgcn_readfirstlane((int)region_map[g]);
         const uint32_t m = order[i];
         const Stat st = stats[i];
-        const bool fixed_on = DYN && (marked[i] & 4u);   // pass 1's marks (an earlier launch)
+        const bool fixed_on = (BPMD_BP_FIXED & 2) && DYN && (marked[i] & 4u);   // pass 1's marks (an earlier launch)
         const uint32_t len = in_len[m];
         const uint32_t tb = task_base[i];
         const uint8_t* p = in + in_off[m];
@@ -1122,7 +1138,8 @@ typedef uint2 uint2_sa __attribute__((aligned(2)));
 constexpr uint32_t RSYM = BPMD_BP_RSYM;
 
 __global__ void __launch_bounds__(256)
-bp_resolve_kernel(const uint32_t* __restrict__ order, const uint32_t* __restrict__ nlong,
+bp_resolve_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                  const uint32_t* __restrict__ order, const uint32_t* __restrict__ nlong,
                   const uint32_t* __restrict__ task_base, const SegTask* __restrict__ tasks,
                   const SegRes* __restrict__ res, const uint16_t* __restrict__ sym, uint8_t* __restrict__ out,
                   const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
@@ -1150,6 +1167,25 @@ bp_resolve_kernel(const uint32_t* __restrict__ order, const uint32_t* __restrict
         while (!fallback) {
             ++nseg;
             const SegRes r = res[t];
+            if (r.status == SEG_DIRECT && r.next > t && r.next != 0xffffffffu) {
+                // a stored block: its bytes from the payload, 16 per lane per step
+                const uint32_t n = r.nsym, room = cap - P;
+                const uint32_t c = n < room ? n : room;
+                const uint8_t* src = in + in_off[m] + (tasks[t].bit >> 3) + 4;
+                uint8_t* dst = o + P;
+                uint32_t j = 16 * lane;
+                for (; j + 16 <= c; j += 1024) *(uint4_ua*)(dst + j) = *(const uint4_ua*)(src + j);
+                for (; j < c; ++j) dst[j] = src[j];   // the last partial 16 bytes (one lane)
+                if (n > room) {
+                    stv = full_status;
+                    olen = cap;
+                    break;
+                }
+                P += n;
+                __builtin_amdgcn_s_waitcnt(0);
+                t = r.next;
+                continue;
+            }
             const uint16_t* sy = sym + tasks[t].sym_off;
             const uint32_t n = r.nsym;
             const uint32_t room = cap - P;   // P <= cap
@@ -1236,7 +1272,7 @@ bp_resolve_kernel(const uint32_t* __restrict__ order, const uint32_t* __restrict
                 t = r.next;
                 continue;
             }
-            if (r.status == SEG_FULL || r.status == SEG_SKIP || r.status == SEG_HANDOFF) {
+            if (r.status == SEG_FULL || r.status == SEG_SKIP || r.status == SEG_HANDOFF || r.status == SEG_DIRECT) {
                 fallback = true;
                 if (lane == 0) {
                     g_bp_fb[0] = m;
@@ -1317,6 +1353,10 @@ bp_chain_kernel(const uint32_t* __restrict__ order, const uint32_t* __restrict__
         uint32_t t = tb, P = 0, k = 0;
         for (;;) {
             const SegRes r = res[t];
+            if (r.status == SEG_DIRECT) {   // (no symbols: this form sends the payload to the wave kernel)
+                pr.flags = 1;
+                break;
+            }
             chp[tb + k] = P;
             chs[tb + k] = tasks[t].sym_off;
             ++k;
@@ -1861,7 +1901,7 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
         return !(e && !strcmp(e, "parallel"));
     }();
     if (serial_resolve) {
-        hipLaunchKernelGGL(bp_resolve_kernel, dim3(8u * cus), dim3(256), 0, s, order, fit, tbase, tasks, res,
+        hipLaunchKernelGGL(bp_resolve_kernel, dim3(8u * cus), dim3(256), 0, s, in, in_off, order, fit, tbase, tasks, res,
                            sym, out, out_off, out_cap, out_len, status, raw, fb, q + 2, q + 1, st);
         if (hipGetLastError() != hipSuccess) return (int)hipErrorUnknown;
     } else {

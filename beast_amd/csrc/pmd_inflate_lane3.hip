@@ -901,6 +901,28 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
         for (int i = 0; i < 7; ++i) tc.Q[i] = 0;
         tc.root = 1;
         srem = 0;
+        if (SEG && kind == bp::KIND_STORED && !skip && nk_bit != 0xffffffffu) {
+            // a stored block whose end is the next candidate's start (this
+            // library's incompressible chunks; runs of Beast's stored blocks):
+            // the resolve copies its bytes straight from the payload
+            // (SEG_DIRECT), the lane decodes nothing.  The next candidate is a
+            // dynamic or fixed header right at the end, or a stored block
+            // whose header byte (BFINAL 0, type 0, padding) precedes its LEN.
+            const uint8_t* pp = pl + byte0;
+            const uint32_t L = (uint32_t)pp[0] | ((uint32_t)pp[1] << 8);
+            const uint32_t NL = (uint32_t)pp[2] | ((uint32_t)pp[3] << 8);
+            const uint32_t e = byte0 + 4 + L;   // the next block's first byte
+            bool direct = (L ^ NL) == 0xffffu && e < pl_len;
+            if (direct)
+                direct = (nk_kind == bp::KIND_DYN || nk_kind == bp::KIND_FIXED)
+                             ? nk_bit == 8 * e
+                             : nk_kind == bp::KIND_STORED && nk_bit == 8 * e + 8 && (pl[e] & 7u) == 0;
+            if (direct) {
+                st = S_DONE;
+                result = bp::SEG_DIRECT;
+                pos = L;
+            }
+        }
     };
     // nx <- the staged block sg (unmasked, tail applied), and the next block
     // is staged (one 16-byte load)
@@ -1512,7 +1534,8 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
             const bool data = !ctl && (enl || emlen || estored);   // produced only with room
             const bool endt = !ctl && !data && st == S_DONE && !fin;
             const bool adv = room && (ctl || data || endt);
-            const uint32_t hand = SEG && result == bp::SEG_HANDOFF ? (nk - msg) << 8 : 0u;
+            const uint32_t hand =
+                SEG && (result == bp::SEG_HANDOFF || result == bp::SEG_DIRECT) ? (nk - msg) << 8 : 0u;
             const uint2 ent = ctl    ? make_uint2(msg, send_new ? TOK_NEW : TOK_EXIT)
                               : data ? make_uint2(elit, estored ? (TOK_STORED | estored)
                                                                 : (enl | (emlen << 3) | (edist << 12)))

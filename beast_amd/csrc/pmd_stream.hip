@@ -533,7 +533,7 @@ int inflate_one(bpmd_stream* s, const uint8_t* in, size_t n, uint8_t* out, size_
 // becomes the leader: it takes up to max_calls queued calls (one per stream),
 // runs them together and wakes their callers.  Calls that arrive while a
 // batch runs form the next one (a group commit: no added latency when a
-// stream is alone -- a batch of one takes the single-call path), and
+// stream is alone -- its batch is one call), and
 // max_delay_us > 0 lets a leader wait that long for more.  Every call's
 // result is its single-call result: the inflate launch runs the same
 // per-stream state machine for each stream (one workgroup per call,
@@ -676,7 +676,7 @@ void fail_all(std::vector<Job*>& jobs, hipStream_t hs)
     for (Job* j : jobs) j->rc = BPMD_R_HIP_ERROR;
 }
 
-// k >= 2 inflate write() calls as one launch.  Block: [ZCall k][inputs]
+// k inflate write() calls as one launch.  Block: [ZCall k][inputs]
 // [Result k][outputs]; one H2D of calls + inputs, the launch, one D2H of the
 // results and outputs (of the results alone, then each call's used output,
 // when the output room is over 4 MiB).
@@ -736,14 +736,12 @@ void inflate_batch(Arena& A, std::vector<Job*>& jobs)
     }
 }
 
+// (a batch of one too: with the batcher on, streams use the leaders'
+// buffers and HIP stream and allocate none of their own -- creating a HIP
+// stream or pinned buffer per connection serializes in the runtime)
 void inflate_exec(Arena& A, std::vector<Job*>& jobs)
 {
     g_bstat[1].fetch_add(1);
-    if (jobs.size() == 1) {
-        Job* j = jobs[0];
-        j->rc = inflate_one(j->s, j->in, j->n, j->out, j->cap, j->flush, j->res);
-        return;
-    }
     inflate_batch(A, jobs);
 }
 
@@ -848,12 +846,7 @@ void deflate_exec(Arena& A, std::vector<Job*>& jobs)
                 g.push_back(jobs[j]);
             }
         g_bstat[3].fetch_add(1);
-        if (g.size() == 1) {
-            Job* j = g[0];
-            j->rc = run_one(j->s, j->s->in.data(), j->s->in.size(), j->out_cap, *j->dout, j->status, j->bits);
-        } else {
-            deflate_group(A, g);
-        }
+        deflate_group(A, g);   // (a group of one too, as inflate_exec)
     }
 }
 

@@ -450,7 +450,7 @@ void bpmd_stream_destroy(bpmd_stream* s);
  * bytes, every z_params field).  A call that finds no batch running takes
  * up to max_calls queued calls (one per stream) and runs them; calls that
  * arrive meanwhile form the next batch, so a lone stream waits for nothing
- * (its batch of one is the single-call path).  max_delay_us > 0: a batch's
+ * (its batch is one call; with the batcher on, streams keep no HIP stream or staging buffers of their own).  max_delay_us > 0: a batch's
  * first call also waits up to that long for more.  max_calls < 2 turns it
  * off.  Default: 256 calls, no delay (environment: BPMD_STREAM_BATCH,
  * BPMD_STREAM_BATCH_DELAY_US). */

@@ -4,6 +4,7 @@ Run under rocprofv3 --kernel-trace --stats for the per-kernel split.
     python scripts/diag_beast_shard.py c5 1 8 [reps]     (leg, level, parts)
     BPMD_LIB=beast_amd/libbeast_pmd_bpdiag.so ... for the scan counters
 """
+import ctypes
 import os
 import sys
 import time
@@ -45,10 +46,14 @@ def main():
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         c = pmd.bp_counters(reset=True)
+        fb = (ctypes.c_uint32 * 8)()
+        pmd.lib().bpmd_diag_bp_fallback(fb)
         ok = int((res.status != 0).sum()) == 0 and torch.equal(out[:ref.numel()], ref)
         print(f"  call {r}: {dt * 1e3:.3f} ms ({ln.astype(np.int64).sum() / 2**30 / dt:.1f} GiB/s) ok={ok} "
               f"bp resolved {c[0]} segments {c[1]} fallback {c[2]} spill {c[3]} | scan regions {c[4]} stored {c[5]} "
-              f"dyn-searched {c[6]} full-checks {c[7]} cyc stage/stored/dyn {c[8]}/{c[9]}/{c[10]}", flush=True)
+              f"dyn-searched {c[6]} full-checks {c[7]} cyc stage/stored/dyn {c[8]}/{c[9]}/{c[10]} | last fallback: "
+              f"msg {fb[0]} seg {fb[1]} status {fb[2]} nsym {fb[3]} cap {fb[4]} next {fb[5]} bit {fb[6]} kind {fb[7]}",
+              flush=True)
 
 
 if __name__ == "__main__":

@@ -292,6 +292,47 @@ def test_stored_block_ending_in_the_last_region():
     assert c[0] == 4 and c[1] == 4 * 18 and c[2] == 0, list(c)[:4]
 
 
+@pytest.mark.parametrize("raw", [False, True])
+def test_stored_segments_copied_from_the_payload(raw):
+    """Round 6: a stored block whose end is the next candidate's start is not
+    decoded by a lane; the resolve copies its bytes from the payload
+    (SEG_DIRECT, pmd_inflate_lane3.hip begin / bp_resolve_kernel).  Runs of
+    hand-made stored blocks (random bytes, 3-5 KB) before a dynamic block,
+    at output capacities that cut inside a stored block, exactly at a block's
+    end, one byte before it, and at the full size: bytes and statuses equal
+    the oracle's serial inflate; with room for the whole output no payload
+    falls back (a small capacity sizes the symbol slots small, bp_stats_kernel,
+    and the dynamic block's segment may then go to the wave kernel)."""
+    import ctypes
+    import zlib
+    pmd = _pmd()
+    rnd = random.Random(11)
+    js = _data("json", 900, 12)
+    co = zlib.compressobj(6, zlib.DEFLATED, -15, 4)
+    dyn = co.compress(js) + co.flush(zlib.Z_SYNC_FLUSH)
+    dyn = dyn[:-4]
+    stored, plain, ends = b"", b"", []
+    for _ in range(24):
+        n = rnd.randrange(3000, 5000)
+        blk = bytes(rnd.getrandbits(8) for _ in range(n))
+        stored += b"\x00" + n.to_bytes(2, "little") + (n ^ 0xFFFF).to_bytes(2, "little") + blk
+        plain += blk
+        ends.append(len(plain))
+    p = stored + dyn
+    full = len(plain) + len(js)
+    cuts = [ends[5], ends[5] - 1, ends[5] + 1, ends[11] + 1234, 77, ends[-1]]
+    c = (ctypes.c_ulonglong * 12)()
+    pmd.lib().bpmd_diag_bp_counters(c, 1)
+    assert pmd.lib().bpmd_set_inflate_kernel(3) == 0
+    try:
+        _check([p] * 4, [full + 16, full, full + 16, full], raw=raw)
+        pmd.lib().bpmd_diag_bp_counters(c, 1)
+        assert c[0] == 4 and c[2] == 0, list(c)[:4]
+        _check([p] * len(cuts), cuts, raw=raw)
+    finally:
+        pmd.lib().bpmd_set_inflate_kernel(0)
+
+
 # ---------------------------------------------------- workspace sizing (r05)
 # A stream's block-parallel decode workspace is sized on its first call (one
 # read-back) or by bpmd_inflate_reserve; payloads over the capacity are
