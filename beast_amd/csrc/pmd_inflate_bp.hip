@@ -370,12 +370,10 @@ __device__ bool dyn_header_ok(const Bits& B, uint32_t b, uint32_t lim)
 #ifndef BPMD_BP_FIXED
 // bit 0: a stored block followed by a fixed block that passes fixed_block_ok
 // is a candidate (round 5: only an empty one); bit 1: pass 2 also searches
-// fixed-block starts after a fixed block's end-of-block code.  Inside a fixed
-// block of literals that pattern shows ~4 times per KiB, and decoding from
-// there resynchronises with the block's own codes within a few symbols, so
-// such a false start passes fixed_block_ok: the pass-2 search is off
-// (profiles/r06l_beast_shard.log: 21-37 % of C5's Beast payloads fell back)
-#define BPMD_BP_FIXED 1
+// fixed-block starts after a fixed block's end-of-block code, checked by
+// fixed_block_ok and fixed_eob_at (without the latter, 21-37 % of C5's
+// Beast payloads fell back: profiles/r06l_beast_shard.log)
+#define BPMD_BP_FIXED 3
 #endif
 constexpr uint32_t FW = 96, FMAX = 6;
 template <class Bits>
@@ -407,6 +405,38 @@ __device__ bool fixed_block_ok(const Bits& B, uint32_t b, uint32_t lim)
         }
     }
     return true;
+}
+
+// Pass 2's fixed-block starts follow a fixed block's end-of-block code
+// (seven zero bits).  Inside a fixed block of literals the same ten bits
+// show about 4 times per KiB (a literal code ending in zeros, the next one
+// starting 010), and decoding from there resynchronises with the block's own
+// codes within a few symbols, so fixed_block_ok cannot tell.  What tells is
+// the stream before: parsed with the fixed code from FBACK bits earlier
+// (also resynchronised by then), a real end-of-block code starts a symbol
+// at t = b - 7; inside a block the symbol boundaries pass over t (the zeros
+// are the tail of one code and the head of the next).
+constexpr uint32_t FBACK = 480;
+template <class Bits>
+__device__ bool fixed_eob_at(const Bits& B, uint32_t from, uint32_t t)
+{
+    uint32_t p = from;
+    for (uint32_t k = 0; k < 160 && p < t; ++k) {
+        const uint32_t c9 = __builtin_bitreverse32(B.peek(p)) >> 23;
+        const uint32_t c7 = c9 >> 2, c8 = c9 >> 1;
+        uint32_t sym;
+        if (c7 <= 23u) { sym = 256u + c7; p += 7; }
+        else if (c8 >= 48u && c8 <= 191u) { sym = c8 - 48u; p += 8; }
+        else if (c8 >= 192u && c8 <= 199u) { sym = 280u + c8 - 192u; p += 8; }
+        else { sym = 144u; p += 9; }
+        if (sym > 256u && sym <= 285u) {   // length extra bits, distance code, its extra bits
+            const uint32_t li = sym - 257u;
+            p += (li < 8u || li == 28u) ? 0u : ((li - 4u) >> 2);
+            const uint32_t d5 = __builtin_bitreverse32(B.peek(p)) >> 27;
+            p += 5u + (d5 < 4u ? 0u : d5 < 30u ? (d5 >> 1) - 1u : 0u);
+        }
+    }
+    return p == t;
 }
 
 // Kraft sum x 128 of four 3-bit code-length-code lengths (0 = unused)
@@ -796,8 +826,21 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
                             uint32_t ok = 0xffffffffu;
                             if (j0 + lane < nc) {
                                 const uint32_t e = list[j0 + lane], b = e & 0x7fffffffu;
-                                if ((e >> 31) ? fixed_block_ok(Lb, b + bias, lim) : dyn_header_ok(Lb, b + bias, lim))
-                                    ok = (b << 1) | (e >> 31);
+                                bool good;
+                                if (e >> 31) {
+                                    good = fixed_block_ok(Lb, b + bias, lim);
+                                    if (good) {
+                                        // (from the stage when it holds bit `from`; the stage's
+                                        // first bit is payload bit -bias)
+                                        const uint32_t from = b > FBACK ? b - FBACK : 0u;
+                                        good = (int32_t)(from + bias) >= 0
+                                                   ? fixed_eob_at(Lb, from + bias, b + bias - 7u)
+                                                   : fixed_eob_at(G, 8 * s + from, 8 * s + b - 7u);
+                                    }
+                                } else {
+                                    good = dyn_header_ok(Lb, b + bias, lim);
+                                }
+                                if (good) ok = (b << 1) | (e >> 31);
                             }
                             for (uint32_t d = 32; d >= 1; d >>= 1) {
                                 const uint32_t y = __shfl_xor(ok, d);
