@@ -787,11 +787,6 @@ struct MsgOut {
     bool overflow;
     uint32_t key;      // masking key, 0 = unmasked: payload byte j ^= key >> 8 (j % 4) (mask.ipp:38-59)
     bool stored;       // the last chunk was written as a stored block
-    // defer (chunk-parallel single write): nothing is written; a Huffman
-    // block's bits stay in the LDS bit buffer (S.win, from bit 0) and
-    // def_bits is their count; a stored block leaves its length in def_bits
-    bool defer;
-    uint32_t def_bits;
 };
 
 __device__ __forceinline__ void put_bytes_global(MsgOut& o, const uint8_t* src_lds, unsigned ob, unsigned nbytes)
@@ -1280,11 +1275,6 @@ emit_block:
         // ---- stored block: 000, pad, LEN, NLEN, bytes (tr_stored_block)
         const unsigned hb = o.cbits + 3 > 8 ? 2u : 1u;
         const unsigned total = hb + 4 + clen;
-        if (o.defer) {   // written by the chunk kernel at its final place
-            o.stored = true;
-            o.def_bits = clen;
-            return;
-        }
         if (o.opos + total > o.cap) { o.overflow = true; return; }
         uint8_t* d = o.dst + o.opos;
         // payload byte opos + j takes key byte (opos + j) % 4 (0 = unmasked)
@@ -1337,7 +1327,7 @@ emit_block:
     const uint32_t incl = wave_scan_incl(nbits);
     const uint32_t tok_bits = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     const uint32_t eob_len = H.codes[EOB] >> 16;
-    const unsigned ob = o.defer ? 0u : (unsigned)((uintptr_t)(o.dst + o.opos) & 3);
+    const unsigned ob = (unsigned)((uintptr_t)(o.dst + o.opos) & 3);
     const uint32_t start_bits = ob * 8 + o.cbits;
     const uint32_t total_bits = o.cbits + hdr_bits + tok_bits + eob_len;   // from the carry's first bit
     const unsigned nbytes = (total_bits + 7) >> 3;
@@ -1414,10 +1404,6 @@ emit_block:
     }
     wave_sync();
     pf.lap(14);
-    if (o.defer) {   // the bits stay in S.win for the chunk kernel
-        o.def_bits = total_bits;
-        return;
-    }
     put_bytes_global(o, (const uint8_t*)ow, ob, nbytes);
     const uint8_t* ob8 = (const uint8_t*)ow;
     o.opos += total_bits >> 3;
@@ -1457,8 +1443,6 @@ deflate_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
         o.overflow = false;
         o.key = P.mask_key ? P.mask_key[i] : 0u;
         o.stored = false;
-        o.defer = false;
-        o.def_bits = 0;
         const uint8_t* msg = in + in_off[i];
         if (len) deflate_chunk<0>(S, msg, 0, len, 0u, P, o, pf);
         // Flush::sync's empty stored block header (000) + pad; 00 00 FF FF stripped
@@ -1569,191 +1553,9 @@ deflate_chunks_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict
         o.overflow = false;
         o.key = 0;
         o.stored = false;
-        o.defer = false;
-        o.def_bits = 0;
         deflate_chunk<HIST>(S, in + in_off[i], c * CHUNK, len, hist, P, o, pf);
         if (lane_id() == 0)
             bits[k] = o.overflow ? 0xFFFFFFFFu : ((o.stored ? 0x80000000u : 0u) | (o.opos * 8 + o.cbits));
-        wave_sync();
-    }
-    pf.flush();
-}
-
-// Chunk-parallel encoding with ONE write of every output byte (round 5;
-// deflate_chunks_kernel + stitch_kernel wrote each block to a scratch slot
-// and then again at its place).  A chunk's block is encoded with its bits
-// left in LDS (MsgOut::defer); its place in the message depends only on
-// where the chunk before it ended, which that chunk's wave publishes in
-// ends[] as soon as it knows it -- before writing its own bytes -- so the
-// wave waits only for that word, then publishes its own end and writes its
-// bytes straight into the payload: stored blocks from the input, Huffman
-// blocks from LDS shifted to their bit offset, the empty stored block before
-// every Huffman chunk but the first (the sync marker of 4.2b), the client
-// mask, and -- the message's last chunk -- Flush::sync's trailer, out_len and
-// status.  The partial byte at a chunk's end travels in ends[] and the next
-// chunk writes it with its own first bits, so no byte is written twice.
-// Forward progress: chunks are taken from the counter in order, so the chunk
-// a wave waits for was taken earlier by a running wave, which waits in turn
-// only for an earlier chunk; the first chunk of a message waits for nothing.
-// ends[k]: bit 63 set when published, bit 62 overflow, bits 8-39 the output
-// bit position after chunk k, bits 0-7 the partial byte there.
-template <int HIST>
-__global__ void __launch_bounds__(64)
-deflate_chunks1_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
-                       const uint32_t* __restrict__ in_len, const uint32_t* __restrict__ items,
-                       const uint32_t* __restrict__ first, const uint32_t* __restrict__ n_items,
-                       unsigned long long* __restrict__ ends, uint8_t* __restrict__ out,
-                       const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
-                       uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t all,
-                       uint32_t* __restrict__ qctr, Params P)
-{
-    __shared__ DefLds<HIST> S;
-    __shared__ uint32_t sh[8];
-    Prof pf;
-    const unsigned lane = lane_id();
-    const uint32_t total = *n_items;
-    auto next = [&]() -> uint32_t {
-        uint32_t v = 0;
-        if (lane == 0) v = atomicAdd(qctr, 1u);
-        return (uint32_t)__shfl((int)v, 0);
-    };
-    constexpr unsigned long long PUB = 1ull << 63, OVF = 1ull << 62;
-    for (uint32_t k = next(); k < total; k = next()) {
-        const uint32_t i = items[k];
-        const uint32_t c = k - first[i];
-        const uint32_t len = in_len[i];
-        const uint32_t nk = (all || len > CHUNK) ? (len + CHUNK - 1) / CHUNK : 0u;
-        const unsigned hist = P.hist_len ? (P.hist_len[i] < (unsigned)HIST ? P.hist_len[i] : (unsigned)HIST) : 0u;
-        const uint8_t* msg = in + in_off[i];
-        MsgOut o;
-        o.dst = nullptr;
-        o.cap = SLOT;
-        o.opos = 0;
-        o.carry = 0;
-        o.cbits = 0;
-        o.overflow = false;
-        o.key = 0;
-        o.stored = false;
-        o.defer = true;
-        o.def_bits = 0;
-        deflate_chunk<HIST>(S, msg, c * CHUNK, len, hist, P, o, pf);
-        const uint8_t* ow8 = (const uint8_t*)S.win;   // the Huffman block's bits, from bit 0
-        const uint32_t cap = out_cap[i];
-        uint8_t* ob = out + out_off[i];
-        const uint32_t key = P.mask_key ? P.mask_key[i] : 0u;
-        auto km = [&](uint32_t p) { return (uint8_t)(key >> (8 * (p & 3))); };
-        const uint32_t L = o.def_bits;
-        // lane 0: the predecessor's end, then this chunk's place and end
-        if (lane == 0) {
-            uint32_t bit = 0, cv = 0;
-            bool ovf = o.overflow;
-            if (c > 0) {
-                // (bounded: a wait that outlived any real chunk -- seconds --
-                // ends the message as need_buffers rather than hanging)
-                unsigned long long v = 0;
-                for (uint32_t spin = 0; spin < (1u << 26); ++spin) {
-                    v = __hip_atomic_load(&ends[k - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (v & PUB) break;
-                    __builtin_amdgcn_s_sleep(2);
-                }
-                if (!(v & PUB)) v = PUB | OVF;
-                ovf = ovf || (v & OVF);
-                bit = (uint32_t)(v >> 8);
-                cv = (uint32_t)v & 0xffu;
-            }
-            uint32_t B = bit >> 3, Pb = 0, start = bit, end = bit, ecv = 0, hdr = 0;
-            if (!ovf) {
-                if (o.stored) {
-                    // 000 at bit, pad, LEN NLEN at Pb, then the bytes; chunk 1
-                    // first gets the marker (hdr 3: 000, pad, 00 00 FF FF, then
-                    // the stored block's 000 and pad in one byte)
-                    Pb = (bit + 3 + 7) >> 3;
-                    hdr = 1;
-                    if (c == 1) {
-                        Pb += 5;
-                        hdr = 3;
-                    }
-                    if (Pb + 4 + L + 1 > cap) ovf = true;
-                    end = (Pb + 4 + L) * 8;
-                } else {
-                    if (c > 0) {   // the empty stored block (sync marker) before the block
-                        Pb = (bit + 3 + 7) >> 3;
-                        if (Pb + 4 + 1 > cap) ovf = true;
-                        start = (Pb + 4) * 8;
-                        hdr = 2;
-                    }
-                    end = start + L;
-                    if (((end + 7) >> 3) + 1 > cap) ovf = true;
-                    if (!ovf && (end & 7)) {
-                        // the partial byte at the end: the block's last bits at its offset
-                        const uint32_t s = start & 7, j = (end >> 3) - (start >> 3);
-                        const uint32_t nb = (L + 7) >> 3;
-                        const uint32_t tj = j < nb ? ow8[j] : 0u, tp = j ? ow8[j - 1] : 0u;
-                        const uint32_t lo = s == 0 ? 0u : (j == 0 ? (hdr ? 0u : cv) : tp >> (8 - s));
-                        ecv = ((tj << s) | lo) & 0xffu;
-                    }
-                }
-            }
-            __hip_atomic_store(&ends[k], PUB | (ovf ? OVF : 0ull) | ((unsigned long long)end << 8) | ecv,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            sh[0] = bit;
-            sh[1] = cv;
-            sh[2] = ovf ? 1u : 0u;
-            sh[3] = Pb;
-            sh[4] = start;
-            sh[5] = end;
-            sh[6] = ecv;
-            sh[7] = hdr;
-            (void)B;
-        }
-        wave_sync();
-        const uint32_t bit = sh[0], cv = sh[1], Pb = sh[3], start = sh[4], end = sh[5], ecv = sh[6], hdr = sh[7];
-        const bool ovf = sh[2] != 0;
-        if (!ovf) {
-            const uint32_t B = bit >> 3;
-            if (hdr) {
-                // the byte holding the predecessor's last bits (and the 000 header
-                // bits), the pad byte if the header crosses it, LEN NLEN
-                const uint32_t Pm = hdr == 3 ? Pb - 5 : Pb;   // the first LEN field after the header bits
-                if (lane == 0) {
-                    ob[B] = (uint8_t)cv ^ km(B);
-                    if (Pm - B == 2) ob[B + 1] = km(B + 1);
-                }
-                if (hdr == 3 && lane < 5) ob[Pm + lane] = (uint8_t)(lane < 2 ? 0x00 : lane < 4 ? 0xff : 0x00) ^ km(Pm + lane);
-                const uint32_t lv = hdr != 2 ? L : 0u;
-                if (lane < 4) {
-                    const uint32_t w = lv | ((~lv & 0xffffu) << 16);
-                    ob[Pb + lane] = (uint8_t)(w >> (8 * lane)) ^ km(Pb + lane);
-                }
-            }
-            if (hdr == 1 || hdr == 3) {
-                const uint8_t* src = msg + c * CHUNK;
-                for (uint32_t j = lane; j < L; j += WAVE) ob[Pb + 4 + j] = src[j] ^ km(Pb + 4 + j);
-            } else {
-                // the block's bits at `start`: full bytes [start >> 3, end >> 3)
-                const uint32_t s = start & 7, B0 = start >> 3, full = (end >> 3) - B0;
-                const uint32_t nb = (L + 7) >> 3;
-                const uint32_t c0 = hdr ? 0u : cv;   // bits already in the first byte
-                for (uint32_t j = lane; j < full; j += WAVE) {
-                    const uint32_t tj = j < nb ? ow8[j] : 0u, tp = j ? ow8[j - 1] : 0u;
-                    const uint32_t lo = s == 0 ? 0u : (j == 0 ? c0 : tp >> (8 - s));
-                    ob[B0 + j] = (uint8_t)(((tj << s) | lo) & 0xffu) ^ km(B0 + j);
-                }
-            }
-        }
-        if (c + 1 == nk && lane == 0) {
-            // Flush::sync's empty stored block header (000) + pad; 00 00 FF FF stripped
-            const uint32_t tbytes = (end & 7) + 3 > 8 ? 2u : 1u;
-            const uint32_t olen = (end >> 3) + tbytes;
-            const bool o2 = ovf || olen > cap;
-            if (!o2) {
-                ob[end >> 3] = (uint8_t)(hdr == 1 ? 0u : ecv) ^ km(end >> 3);
-                if (tbytes == 2) ob[(end >> 3) + 1] = km((end >> 3) + 1);
-            }
-            out_len[i] = o2 ? 0u : olen;
-            if (P.out_bits) P.out_bits[i] = o2 ? 0u : end;
-            status[i] = o2 ? ST_NEED_BUFFERS : ST_OK;
-        }
         wave_sync();
     }
     pf.flush();
@@ -1765,14 +1567,13 @@ stitch_kernel(const uint32_t* __restrict__ in_len, uint32_t n, uint32_t all, con
               const uint8_t* __restrict__ temp, const uint32_t* __restrict__ bits, uint8_t* __restrict__ out,
               const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
               uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t* __restrict__ out_bits,
-              const uint32_t* __restrict__ mask_key, uint32_t empty_only)
+              const uint32_t* __restrict__ mask_key)
 {
     const unsigned lane = lane_id();
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
         const uint32_t len = in_len[i];
         if (!all && len <= CHUNK) continue;
         const uint32_t nk = chunk_count(len, all != 0), f = first[i];
-        if (empty_only && nk) continue;   // the single-write chunk kernel finished it
         uint8_t* o = out + out_off[i];
         const uint32_t cap = out_cap[i];
         const uint32_t key = mask_key ? mask_key[i] : 0u;
@@ -1898,12 +1699,6 @@ int launch_single(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_
 }  // namespace
 
 namespace {
-std::atomic<int> g_single_write{-1};   // -1 from BPMD_DEFLATE_STITCH, 0 stitch, 1 single write
-}  // namespace
-// tests / A/B: the single-write chunk kernel (1) or the stitch (0)
-extern "C" void bpmd_diag_set_deflate_single_write(int on) { g_single_write.store(on ? 1 : 0); }
-
-namespace {
 // tune: null, or deflate_stream::tune's (good_length, max_lazy, nice_length,
 // max_chain) (deflate_stream.ipp:307-317) replacing the level's table row;
 // the level still picks the parser, and the chain keeps the engine's caps
@@ -1982,18 +1777,11 @@ int deflate_impl(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_l
         return 0;
     }
     // workspace: first[n + 1] | items[total] | bits[total] | slots[total] | scan temp
-    // (single write: ends[total] in place of bits and slots)
-    // the single-write chunk kernel (BPMD_DEFLATE_STITCH=0) measured slower
-    // than the stitch: a chunk's wave waits, holding its CU slot, for the
-    // chunk before it to finish encoding (C4 26.6 -> 23.8, C5 L1 27.6 -> 25.5
-    // GiB/s, profiles/r05k_ab_single_write.log); the stitch stays the default
-    int sm = g_single_write.load();
-    if (sm < 0) {
-        const char* e = getenv("BPMD_DEFLATE_STITCH");
-        sm = e && e[0] == '0' ? 1 : 0;
-        g_single_write.store(sm);
-    }
-    const bool stitch = sm == 0;
+    // (round 5's single-write chunk kernel, which placed each chunk's block
+    // without the stitch's second write, measured slower -- a chunk's wave
+    // waits, holding its CU slot, for the chunk before it to finish encoding:
+    // C4 26.6 -> 23.8, C5 L1 27.6 -> 25.5 GiB/s, profiles/r05k_ab_single_write.log
+    // -- and was removed in round 6)
     size_t cub_bytes = 0;
     hipcub::CountingInputIterator<uint32_t> idx(0);
     hipcub::TransformInputIterator<uint32_t, ChunkCountOp, hipcub::CountingInputIterator<uint32_t>> counts(
@@ -2005,8 +1793,8 @@ int deflate_impl(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_l
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t o_first = 0, o_items = up(o_first + 4ull * (n + 1)),
                  o_bits = up(o_items + 4ull * total),
-                 o_slots = up(o_bits + (stitch ? 4ull : 8ull) * total),
-                 o_cub = up(o_slots + (stitch ? (size_t)SLOT * total : 0)), bytes = up(o_cub + cub_bytes);
+                 o_slots = up(o_bits + 4ull * total),
+                 o_cub = up(o_slots + (size_t)SLOT * total), bytes = up(o_cub + cub_bytes);
     uint8_t* ws = (uint8_t*)bpmd_internal_scratch(stream, bytes, 2);
     if (!ws) return (int)hipErrorOutOfMemory;
     uint32_t* first = (uint32_t*)(ws + o_first);
@@ -2030,16 +1818,8 @@ int deflate_impl(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_l
         constexpr int H = decltype(hist_tag)::value;
         const unsigned per_cu = (160u * 1024u) / (unsigned)sizeof(DefLds<H>);
         const unsigned grid = total < (uint32_t)cus * per_cu ? total : (unsigned)cus * per_cu;
-        if (stitch) {
-            hipLaunchKernelGGL(deflate_chunks_kernel<H>, dim3(grid), dim3(64), 0, stream, in, in_off, in_len, items,
-                               first, d_total, slots, bits, d_total + 32, P);
-        } else {
-            unsigned long long* ends = (unsigned long long*)(ws + o_bits);
-            hipError_t e2 = hipMemsetAsync(ends, 0, 8ull * total, stream);
-            if (e2 != hipSuccess) return (int)e2;
-            hipLaunchKernelGGL(deflate_chunks1_kernel<H>, dim3(grid), dim3(64), 0, stream, in, in_off, in_len, items,
-                               first, d_total, ends, out, out_off, out_cap, out_len, status, all, d_total + 32, P);
-        }
+        hipLaunchKernelGGL(deflate_chunks_kernel<H>, dim3(grid), dim3(64), 0, stream, in, in_off, in_len, items,
+                           first, d_total, slots, bits, d_total + 32, P);
         return 0;
     };
     if (total) {
@@ -2048,12 +1828,11 @@ int deflate_impl(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_l
                           : launch_chunks(std::integral_constant<int, CHUNK_HIST>{});
         if (e) return e;
     }
-    // the stitch: every chunked message (BPMD_DEFLATE_STITCH=1, round 4), or
-    // only the empty messages of a takeover batch (no chunk to finish them)
-    if (stitch || all) {
+    // the stitch: every chunked message (and the empty messages of a takeover batch)
+    {
         const unsigned sgrid = n < (uint32_t)cus * 16 ? n : (unsigned)cus * 16;
         hipLaunchKernelGGL(stitch_kernel, dim3(sgrid), dim3(64), 0, stream, in_len, n, all, first, slots, bits, out,
-                           out_off, out_cap, out_len, status, out_bits, mask_key, stitch ? 0u : 1u);
+                           out_off, out_cap, out_len, status, out_bits, mask_key);
     }
     return (int)hipGetLastError();
 }

@@ -139,40 +139,3 @@ def test_gpu_inflate_of_gpu_deflate_full_batch():
     torch.cuda.synchronize()
     assert int((r.status != 0).sum()) == 0
     assert torch.equal(r.out.data[: n * 4096].view(n, 4096), src.data[: n * 4096].view(n, 4096))
-
-
-@pytest.mark.parametrize("level", [1, 6])
-def test_single_write_chunk_path_equals_stitch(level):
-    """The single-write chunk kernel (measured slower, off by default;
-    bpmd_diag_set_deflate_single_write) produces the same payload bytes as the
-    stitch, masked client payloads and capacity cuts included, and they
-    inflate back."""
-    import torch
-    from beast_amd import pmd
-    rng = random.Random(11 + level)
-    msgs = []
-    for _ in range(120):
-        k = rng.choice(["json", "corpus1", "random", "binary"])
-        s = rng.choice([4097, 9000, 16384, 65536, 100000])
-        d, _, _ = synth.make_batch(k, [s], seed=rng.randrange(1 << 30))
-        msgs.append(bytes(d[:s]))
-    caps = [O.upper_bound(len(m)) if i % 9 else len(m) // 2 for i, m in enumerate(msgs)]
-    src = pmd.Batch.from_host(msgs)
-    keys = torch.randint(-2**31, 2**31 - 1, (len(msgs),), dtype=torch.int32)
-    outs = []
-    L = pmd.lib()
-    try:
-        for single in (0, 1):
-            L.bpmd_diag_set_deflate_single_write(single)
-            a = pmd.deflate_batch(src, level=level, out_cap=torch.tensor(caps, dtype=torch.int32))
-            b = pmd.write_batch(src, key=keys, level=level)
-            torch.cuda.synchronize()
-            outs.append((a.status.cpu().tolist(), a.out.to_host(), b.status.cpu().tolist(), b.out.to_host()))
-    finally:
-        L.bpmd_diag_set_deflate_single_write(0)
-    assert outs[0] == outs[1]
-    st, pl = outs[1][0], outs[1][1]
-    ok = [i for i in range(len(msgs)) if st[i] == 0]
-    assert len(ok) > 100 and all(i % 9 == 0 for i in range(len(msgs)) if st[i] != 0)
-    _check_roundtrip([msgs[i] for i in ok], [pl[i] for i in ok], [st[i] for i in ok])
-    assert all(st[i] == 1 and pl[i] == b"" for i in range(len(msgs)) if st[i] != 0)
