@@ -591,7 +591,23 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
             // MARK_SPAN + R of the payload's end -- a foreign encoder's payload
             // that flushed once near its start is searched; bit 2
             // a stored block with data, which turns on the fixed-block search)
-            if (((marked[ri] & 3u) | (BPMD_BP_MARK_END ? 0u : 2u)) == 3u || (gl - task_base[ri]) % dyn_stride != 0) {
+            // The stride (BPMD_BP_DYN_STRIDE, else per payload): a payload with
+            // stored data blocks (near-random data: a Beast peer's stored and
+            // fixed runs, bit 2) is searched in one region per 4 KiB whatever
+            // the region size, so a small batch's fine regions (R down to
+            // R_MIN for an 8-way shard) do not multiply the search; the
+            // other payloads in every region (C4's dynamic blocks of ~350
+            // bytes need the candidates).  C5 8-way Beast shards L1 / L6 8.8 /
+            // 16.0 -> 8.1 / 9.4 ms at stride 4 everywhere, while C4's rose
+            // 16.1 -> 20.6 ms and the whole C5 batch (R = 4 KiB) fell 60 -> 48
+            // GiB/s (profiles/r06w_stride_sweep.log)
+            // (the last region, which also takes the payload's remainder, is
+            // always searched)
+            const uint32_t mk = marked[ri];
+            const Stat sr = stats[ri];
+            const uint32_t kr = gl - task_base[ri];
+            const uint32_t ds = dyn_stride > 1 ? dyn_stride : (mk & 4u) && sr.R < 4096u ? 4096u / sr.R : 1u;
+            if (((mk & 3u) | (BPMD_BP_MARK_END ? 0u : 2u)) == 3u || (kr % ds != 0 && kr + 1 != sr.regions)) {
                 tasks[gl].kind = KIND_NONE;
             } else {
                 // a region inside the data of a stored block pass 1 found (one
@@ -1907,7 +1923,7 @@ extern "C" int bpmd_internal_inflate_bp(const uint8_t* in, const uint64_t* in_of
     static const uint32_t dyn_stride = [] {
         const char* e = getenv("BPMD_BP_DYN_STRIDE");
         const uint32_t v = e ? (uint32_t)strtoul(e, nullptr, 10) : 0u;
-        return v ? v : 1u;
+        return v ? v : 1u;   // 1: the per-payload stride (bp_scan_kernel)
     }();
     hipLaunchKernelGGL(bp_scan_kernel<false>, dim3(scan_wgs), dim3(64 * SCAN_WAVES), 0, s, in, in_off, in_len, order,
                        rmap, fit + 1, st, tbase, tasks, marked, dyn_stride);
