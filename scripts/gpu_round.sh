@@ -18,6 +18,8 @@
 #   diag         lane-kernel loop counters (prof build) -> gpurun_out/<TAG>_diag_lane3.txt
 #   e2e          PCIe-inclusive rates                -> gpurun_out/<TAG>_e2e.json
 #   shards       one 8-way shard's kernels per leg   -> gpurun_out/<TAG>_shards.log
+#   bshard       one 8-way shard of C5 Beast payloads, L1 and L6, kernel trace -> gpurun_out/prof_bshard_<TAG>/
+#   n2           the N2 harness at 64 threads, 1 and 16 KiB, GPU and CPU codec -> gpurun_out/<TAG>_n2_sweep.log
 #   py:<script>  python scripts/<script> (args in PY_ARGS) -> gpurun_out/<TAG>_<script>.log
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -84,6 +86,12 @@ for s in "$@"; do
     shards)
       step shards
       TAG=$TAG bash scripts/prof_shards.sh > gpurun_out/${TAG}_shards.log 2>&1 || { tail -10 gpurun_out/${TAG}_shards.log; exit 23; } ;;
+    bshard)
+      step bshard
+      for L in 1 6; do TAG=$TAG LEVEL=$L bash scripts/prof_beast_shard.sh > gpurun_out/${TAG}_bshard_l$L.log 2>&1 || { tail -10 gpurun_out/${TAG}_bshard_l$L.log; exit 25; }; head -6 gpurun_out/${TAG}_bshard_l$L.log | cut -c1-160; done ;;
+    n2)
+      step n2
+      TAG=$TAG THREADS="${THREADS:-64}" bash scripts/n2_sweep.sh || exit 26 ;;
     py:*)
       sc=${s#py:}; step "py $sc"
       timeout -k 10 ${PY_TIMEOUT:-300} python -u scripts/$sc $PY_ARGS > gpurun_out/${TAG}_${sc%.py}.log 2>&1 || { tail -30 gpurun_out/${TAG}_${sc%.py}.log; exit 24; }

@@ -11,7 +11,7 @@ PY
 cd /tmp && export TMPDIR=/tmp
 OUT=$R/gpurun_out/prof_n2_$TAG
 mkdir -p $OUT
-timeout -k 10 300 rocprofv3 --kernel-trace --hip-trace --stats --output-format csv -d $OUT/run -o trace \
+BATCH_STREAMS_ONLY_BATCHED=${ONLY_BATCHED:-0} timeout -k 10 300 rocprofv3 --kernel-trace --hip-trace --stats --output-format csv -d $OUT/run -o trace \
   -- $R/tests/cpp/_build/batch_streams ${T:-64} ${MSGS:-24} ${SIZE:-1024} > $OUT/log.txt 2> $OUT/err.log || { tail -5 $OUT/err.log; exit 3; }
 cat $OUT/log.txt
 for f in kernel_stats hip_api_stats; do
