@@ -134,10 +134,10 @@ bp_stats_kernel(const uint32_t* __restrict__ in_len, const uint32_t* __restrict_
         s.regions = na;
         s.R = (uint32_t)R;
         s.F16 = (uint32_t)((e16 * 5) >> 2);
-        // slots: span to the candidate after next (rounded up to bytes; the
-        // spans add up to at most 2 (len + na)) x F16, plus SLACK each, after
-        // the payload's guard
-        w = ((((unsigned long long)2 * (len + na)) * s.F16) >> 16) + (unsigned long long)SLACK * na + SYM_GUARD + 64;
+        // slots: span to the third candidate after it (rounded up to bytes;
+        // the spans add up to at most 3 (len + na)) x F16, plus SLACK each,
+        // after the payload's guard
+        w = ((((unsigned long long)3 * (len + na)) * s.F16) >> 16) + (unsigned long long)SLACK * na + SYM_GUARD + 64;
     }
     st[i] = s;
     regions[i] = na;
@@ -607,7 +607,11 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
             const Stat sr = stats[ri];
             const uint32_t kr = gl - task_base[ri];
             const uint32_t ds = dyn_stride > 1 ? dyn_stride : (mk & 4u) && sr.R < 4096u ? 4096u / sr.R : 1u;
-            if (((mk & 3u) | (BPMD_BP_MARK_END ? 0u : 2u)) == 3u || (kr % ds != 0 && kr + 1 != sr.regions)) {
+            // (a region the stride passes over still gets the fixed-block
+            // search when the payload has it: that one is cheap)
+            const bool fixed_only = kr % ds != 0 && kr + 1 != sr.regions;
+            if (((mk & 3u) | (BPMD_BP_MARK_END ? 0u : 2u)) == 3u ||
+                (fixed_only && !((BPMD_BP_FIXED & 2) && (mk & 4u)))) {
                 tasks[gl].kind = KIND_NONE;
             } else {
                 // a region inside the data of a stored block pass 1 found (one
@@ -646,6 +650,12 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
         const uint32_t m = order[i];
         const Stat st = stats[i];
         const bool fixed_on = (BPMD_BP_FIXED & 2) && DYN && (marked[i] & 4u);   // pass 1's marks (an earlier launch)
+        // the dynamic-header search only in every ds-th region of a payload
+        // with stored data blocks (and its last); the others search fixed
+        // starts only (the screening above)
+        const uint32_t kq = g - task_base[i];
+        const uint32_t dsq = dyn_stride > 1 ? dyn_stride : (marked[i] & 4u) && st.R < 4096u ? 4096u / st.R : 1u;
+        const bool dyn_on = kq % dsq == 0 || kq + 1 == st.regions;
         const uint32_t len = in_len[m];
         const uint32_t tb = task_base[i];
         const uint8_t* p = in + in_off[m];
@@ -777,7 +787,7 @@ bp_scan_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
                             uint64_t mk = ~lo & ~(lo >> 1) & (lo >> 2);
                             mk &= ~((lo >> 4) & (lo >> 5) & (lo >> 6) & (lo >> 7));
                             mk &= ~((lo >> 9) & (lo >> 10) & (lo >> 11) & (lo >> 12));
-                            uint32_t cand = (uint32_t)mk;
+                            uint32_t cand = dyn_on ? (uint32_t)mk : 0u;
                             if (first >= b1) cand = 0;
                             else if (b1 - first < 32) cand &= (1u << (b1 - first)) - 1u;
                             // fixed-block starts after a fixed block (round 6): seven zero
@@ -1122,44 +1132,52 @@ bp_slots_kernel(const uint32_t* __restrict__ in_len, const uint32_t* __restrict_
         const uint32_t len = in_len[order[i]];
         const uint32_t tb = task_base[i];
         uint64_t run = word_base[i] + SYM_GUARD;
-        // A slot reaches to the candidate after next: a false candidate (a
-        // random LEN / NLEN whose LEN happens to land on a real block start,
-        // ~1 per GiB of binary payload) that precedes a region's real one
-        // must not size the real segment's slot to its own short span.
-        uint32_t n1 = 8 * len, n2 = 8 * len;   // the two next candidates' bits, from the chunks after
+        // A slot reaches to the third candidate after it: a false candidate
+        // (a random LEN / NLEN whose LEN happens to land on a real block
+        // start, ~1 per GiB of binary payload; a fixed-block start the checks
+        // let through) that precedes a region's real one must not size the
+        // real segment's slot to its own short span.  (Round 5 reached to the
+        // second: one 8-way C5 shard of Beast payloads in two then sent one
+        // payload to the wave kernel, +4 to +7 ms, profiles/r06g_shard_fallbacks.log.)
+        uint32_t n1 = 8 * len, n2 = 8 * len, n3 = 8 * len;   // the three next candidates' bits, from the chunks after
         const uint32_t nch = (st.regions + 63) / 64;
-        auto two_min = [](uint32_t& a1, uint32_t& a2, uint32_t b1, uint32_t b2) {
-            const uint32_t lo = a1 < b1 ? a1 : b1, hi = a1 < b1 ? b1 : a1;
-            const uint32_t m = a2 < b2 ? a2 : b2;
-            a1 = lo;
-            a2 = hi < m ? hi : m;
+        // (a1, a2, a3) <- the three smallest of (a1, a2, a3) and (b1, b2, b3), ascending
+        auto three_min = [](uint32_t& a1, uint32_t& a2, uint32_t& a3, uint32_t b1, uint32_t b2, uint32_t b3) {
+            auto ins = [&](uint32_t v) {
+                if (v < a3) a3 = v;
+                if (a3 < a2) { const uint32_t t = a2; a2 = a3; a3 = t; }
+                if (a2 < a1) { const uint32_t t = a1; a1 = a2; a2 = t; }
+            };
+            ins(b1);
+            ins(b2);
+            ins(b3);
         };
-        // chunks from the last to the first (suffix scans of the two smallest
+        // chunks from the last to the first (suffix scans of the three smallest
         // candidate bits), slot offsets assigned afterwards from the first
         SegTask* vt = tasks + tb;
         for (uint32_t c = nch; c-- > 0;) {
             const uint32_t k = c * 64 + lane;
             const bool v = k < st.regions && vt[k].kind != KIND_NONE;
             const uint32_t b = v ? vt[k].bit : 0xffffffffu;
-            uint32_t s1 = b, s2 = 0xffffffffu;   // inclusive suffix: the two smallest from k on
+            uint32_t s1 = b, s2 = 0xffffffffu, s3 = 0xffffffffu;   // inclusive suffix: the three smallest from k on
             for (uint32_t d = 1; d < 64; d <<= 1) {
-                const uint32_t y1 = __shfl_down(s1, d), y2 = __shfl_down(s2, d);
-                if (lane + d < 64) two_min(s1, s2, y1, y2);
+                const uint32_t y1 = __shfl_down(s1, d), y2 = __shfl_down(s2, d), y3 = __shfl_down(s3, d);
+                if (lane + d < 64) three_min(s1, s2, s3, y1, y2, y3);
             }
-            // the two candidates after k: lane k + 1's suffix, then the chunks after
-            uint32_t a1 = __shfl_down(s1, 1), a2 = __shfl_down(s2, 1);
-            if (lane == 63) a1 = a2 = 0xffffffffu;
-            two_min(a1, a2, n1, n2);
+            // the three candidates after k: lane k + 1's suffix, then the chunks after
+            uint32_t a1 = __shfl_down(s1, 1), a2 = __shfl_down(s2, 1), a3 = __shfl_down(s3, 1);
+            if (lane == 63) a1 = a2 = a3 = 0xffffffffu;
+            three_min(a1, a2, a3, n1, n2, n3);
             if (v) {
-                const uint32_t after = a2 < 8 * len ? a2 : 8 * len;
+                const uint32_t after = a3 < 8 * len ? a3 : 8 * len;
                 const uint32_t span = after > b ? (after - b + 7) >> 3 : 1u;
                 vt[k].sym_cap = (uint32_t)(((uint64_t)span * st.F16) >> 16) + SLACK;
             }
-            const uint32_t f1 = __shfl(s1, 0), f2 = __shfl(s2, 0);
-            uint32_t c1 = f1, c2 = f2;
-            two_min(c1, c2, n1, n2);
+            uint32_t c1 = __shfl(s1, 0), c2 = __shfl(s2, 0), c3 = __shfl(s3, 0);
+            three_min(c1, c2, c3, n1, n2, n3);
             n1 = c1;
             n2 = c2;
+            n3 = c3;
         }
         __builtin_amdgcn_s_waitcnt(0);
         __builtin_amdgcn_wave_barrier();
@@ -1757,7 +1775,8 @@ extern "C" int bpmd_internal_bp_reserve(hipStream_t s, unsigned long long in_byt
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return (int)hipErrorNoDevice;
     const unsigned long long t = in_bytes / R_MIN + msgs;
-    const unsigned long long w = (5 * out_bytes) / 2 + (10ull + SLACK) * t + (SYM_GUARD + 64ull) * msgs;
+    // (bp_stats_kernel: slots of 3 (len + regions) x F16 symbols, F16 = 1.25 x cap / len)
+    const unsigned long long w = (15 * out_bytes) / 4 + (15ull + SLACK) * t + (SYM_GUARD + 64ull) * msgs;
     std::lock_guard<std::mutex> lk(g_bp_mu);
     BpCaps* c = caps_for(dev, s);
     if (!c) return (int)hipErrorOutOfMemory;

@@ -1,7 +1,7 @@
 """Beast-produced payloads (host zlib = Beast's deflate_stream) on one shard
 of C4 (L6) or C5 (L1 / L6): timing per call and the block-parallel counters.
 Run under rocprofv3 --kernel-trace --stats for the per-kernel split.
-    python scripts/diag_beast_shard.py c5 1 8 [reps]     (leg, level, parts)
+    python scripts/diag_beast_shard.py c5 1 8 [reps] [shard]     (leg, level, parts)
     BPMD_LIB=beast_amd/libbeast_pmd_bpdiag.so ... for the scan counters
 """
 import ctypes
@@ -21,11 +21,12 @@ from beast_amd import pmd, shard, synth  # noqa: E402
 def main():
     leg, level, parts = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
     reps = int(sys.argv[4]) if len(sys.argv) > 4 else 3
+    which = int(sys.argv[5]) if len(sys.argv) > 5 else 0   # the shard (of `parts`)
     if leg == "c4":
         lens_all, kind, seed = synth.zipf_sizes(bench.C4_MSGS, bench.SEED_C4), "json", bench.SEED_C4
     else:
         lens_all, kind, seed = np.full(bench.C5_MSGS, 65536, np.uint32), "binary", bench.SEED_C5
-    a, b = shard.byte_balanced_ranges(lens_all, parts)[0] if parts > 1 else (0, len(lens_all))
+    a, b = shard.byte_balanced_ranges(lens_all, parts)[which] if parts > 1 else (0, len(lens_all))
     lens = lens_all[a:b]
     raw, off, ln = synth.make_batch(kind, lens, seed=seed, first=a)
     payloads, _ = bench.beast_payloads(raw, off, ln, level)
