@@ -184,8 +184,11 @@ int main(int argc, char** argv)
     return 0;
 #else
     unsigned long long st[4];
+    // BATCH_STREAMS_ONLY_BATCHED=1 (profiling): the batched run alone
+    const char* ob = std::getenv("BATCH_STREAMS_ONLY_BATCHED");
+    const bool only_batched = ob && ob[0] == '1';
     bpmd_stream_batching(0, 0);
-    const Run a = run_all(T, M, bytes);
+    const Run a = only_batched ? Run{} : run_all(T, M, bytes);
     if (!a.engine) return 3;
     bpmd_stream_batch_stats(st, 1);
     bpmd_stream_batching(256, 0);
@@ -197,7 +200,7 @@ int main(int argc, char** argv)
         std::fprintf(stderr, "round trip mismatch: unbatched %d batched %d\n", (int)a.ok, (int)b.ok);
         return 1;
     }
-    for (int t = 0; t < T; ++t)
+    for (int t = 0; t < T && !only_batched; ++t)
         if (a.payloads[t] != b.payloads[t]) {
             std::fprintf(stderr, "thread %d: batched payloads differ from unbatched\n", t);
             return 1;
