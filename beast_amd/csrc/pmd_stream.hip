@@ -611,6 +611,7 @@ int batch_max()
 
 class Coalescer {
   public:
+    explicit Coalescer(int dev) : dev_(dev) {}
     template <class Exec>
     void run(Job* j, int max_calls, Exec&& exec)
     {
@@ -640,7 +641,13 @@ class Coalescer {
                 it = q_.erase(it);
             }
             lk.unlock();
+            // the coalescer's device (its streams' state lives there), whatever
+            // this thread had current
+            int prev = -1;
+            (void)hipGetDevice(&prev);
+            if (prev != dev_) (void)hipSetDevice(dev_);
             exec(arena_, take);
+            if (prev != dev_ && prev >= 0) (void)hipSetDevice(prev);
             lk.lock();
             for (Job* t : take) t->done = true;
             busy_ = false;
@@ -654,18 +661,22 @@ class Coalescer {
     std::deque<Job*> q_;
     bool busy_ = false;
     Arena arena_;
+    int dev_;
 };
 
-// process-lifetime objects (never destroyed: HIP may be torn down first)
-Coalescer& inflate_coalescer()
+// one pair per device: a stream's device state lives on the device its
+// owner had current, and calls only batch with calls of the same device.
+// Process-lifetime objects (never destroyed: HIP may be torn down first).
+constexpr int MAX_DEV = 64;
+Coalescer* coalescer(int dev, bool inflate)
 {
-    static Coalescer* c = new Coalescer();
-    return *c;
-}
-Coalescer& deflate_coalescer()
-{
-    static Coalescer* c = new Coalescer();
-    return *c;
+    static std::mutex mu;
+    static Coalescer* tab[2][MAX_DEV] = {};
+    if (dev < 0 || dev >= MAX_DEV) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    Coalescer*& c = tab[inflate ? 0 : 1][dev];
+    if (!c) c = new (std::nothrow) Coalescer(dev);
+    return c;
 }
 
 constexpr size_t up256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -863,7 +874,10 @@ int inflate_call(bpmd_stream* s, const uint8_t* in, size_t n, uint8_t* out, size
     j.out = out;
     j.cap = cap;
     j.flush = flush;
-    inflate_coalescer().run(&j, mx, inflate_exec);
+    int dev = 0;
+    Coalescer* c = hipGetDevice(&dev) == hipSuccess ? coalescer(dev, true) : nullptr;
+    if (!c) return inflate_one(s, in, n, out, cap, flush, res);
+    c->run(&j, mx, inflate_exec);
     res = j.res;
     return j.rc;
 }
@@ -877,7 +891,10 @@ int run_flush(bpmd_stream* s, size_t out_cap, std::vector<uint8_t>& out, int32_t
     j.s = s;
     j.out_cap = out_cap;
     j.dout = &out;
-    deflate_coalescer().run(&j, mx, deflate_exec);
+    int dev = 0;
+    Coalescer* c = hipGetDevice(&dev) == hipSuccess ? coalescer(dev, false) : nullptr;
+    if (!c) return run_one(s, s->in.data(), s->in.size(), out_cap, out, status, bits);
+    c->run(&j, mx, deflate_exec);
     status = j.status;
     bits = j.bits;
     return j.rc;
