@@ -21,6 +21,9 @@
 #   bshard       one 8-way shard of C5 Beast payloads, L1 and L6, kernel trace -> gpurun_out/prof_bshard_<TAG>/
 #   n2           the N2 harness at 64 threads, 1 and 16 KiB, GPU and CPU codec -> gpurun_out/<TAG>_n2_sweep.log
 #   py:<script>  python scripts/<script> (args in PY_ARGS) -> gpurun_out/<TAG>_<script>.log
+# Companions run on their own: scripts/ab_legs.sh (A/B of library variants on the
+# C4 / C5 legs), scripts/ktrace.sh (C2-only kernel trace), scripts/prof_n2.sh (N2
+# harness under rocprofv3 with the HIP API trace).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${TAG:-r06}
