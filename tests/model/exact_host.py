@@ -77,10 +77,15 @@ def build():
     src = open(KSRC).read()
     body = src[:src.index("// LDS tiers by message length")]
     body = body.replace('#include "pmd_common.h"', "")
-    with open(GEN, "w") as f:
+    # per-process names and an atomic rename: parallel test workers (pytest -n)
+    # may build at once, and one must never load a half-written library
+    gen, tmp = "%s.%d.cpp" % (GEN[:-4], os.getpid()), "%s.%d.tmp" % (LIB, os.getpid())
+    with open(gen, "w") as f:
         f.write(SHIM + body + DRIVER)
-    subprocess.run([CLANG, "-O2", "-std=c++17", "-shared", "-fPIC", "-Wno-unused-function", GEN, "-o", LIB],
+    subprocess.run([CLANG, "-O2", "-std=c++17", "-shared", "-fPIC", "-Wno-unused-function", gen, "-o", tmp],
                    check=True)
+    os.replace(tmp, LIB)
+    os.remove(gen)
     return LIB
 
 

@@ -27,7 +27,9 @@ def build():
     deps = [SRC, os.path.join(CSRC, "lz_core.h")]
     if os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(d) for d in deps):
         return LIB
-    subprocess.run(["g++", "-O2", "-shared", "-fPIC", "-I", CSRC, SRC, "-o", LIB], check=True)
+    tmp = "%s.%d.tmp" % (LIB, os.getpid())   # atomic under parallel test workers
+    subprocess.run(["g++", "-O2", "-shared", "-fPIC", "-I", CSRC, SRC, "-o", tmp], check=True)
+    os.replace(tmp, LIB)
     return LIB
 
 
