@@ -172,6 +172,26 @@ LZ_HD bool incompressible(unsigned hits, unsigned chunk_bytes)
 #define BPMD_INCOMP_STORED 1
 #endif
 constexpr bool INCOMP_STORED = BPMD_INCOMP_STORED != 0;
+// Round 6: the block choice of a chunk of a multi-chunk message.  Beast keeps
+// a Huffman block whenever it is smaller than the stored one
+// (tr_flush_block, deflate_stream.ipp:1478: stored_len + 4 <= opt_lenb).
+// Here it must also save 1/2^BPMD_MIN_GAIN_SHIFT of the chunk (256 bytes of
+// 4 KiB at 4): a stored chunk inflates as one copy (SEG_DIRECT),
+// a Huffman chunk of near-random bytes one symbol at a time on one lane
+// (~2 ms per 4 KiB), and a chunk that saves under ~6 % is that kind.  Messages
+// of one chunk keep Beast's rule.  0 restores it everywhere.  C5 (near-random
+// binary, profiles/r06m_ab_min_gain.log), shift 0 / 5 / 4 / 3: size 1.0077 /
+// 1.0091 / 1.0128 / 1.0158x Beast's at L1, deflate 98.6 / 102.9 / 109.0 /
+// 112.6 GiB/s, inflate 174 / 177 / 192 / 248 GiB/s.  JSON chunks save 60-70 %
+// and never reach the rule.
+#ifndef BPMD_MIN_GAIN_SHIFT
+#define BPMD_MIN_GAIN_SHIFT 4
+#endif
+LZ_HD bool chunk_stored(unsigned clen, unsigned long long best_bytes, bool multi_chunk)
+{
+    const unsigned slack = (BPMD_MIN_GAIN_SHIFT && multi_chunk) ? clen >> BPMD_MIN_GAIN_SHIFT : 0u;
+    return (unsigned long long)clen + 4 <= best_bytes + slack;
+}
 
 LZ_HD uint32_t chain_hash(uint32_t w, unsigned avail, unsigned hbits)
 {

@@ -1266,7 +1266,7 @@ __device__ void deflate_chunk(DefLds<HIST>& S, const uint8_t* msg, unsigned base
         const uint32_t fix_b = (fix + 7) >> 3;
         if (P.strategy == 4) opt_b = fix_b + 1;
         const uint32_t best = opt_b < fix_b ? opt_b : fix_b;
-        kind = (clen + 4 <= best) ? 0u : (fix_b <= opt_b ? 1u : 2u);
+        kind = chunk_stored(clen, best, len > CHUNK) ? 0u : (fix_b <= opt_b ? 1u : 2u);
         pf.lap(10);
     }
 

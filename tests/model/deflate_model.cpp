@@ -258,7 +258,7 @@ static std::vector<uint8_t> encode(const uint8_t* msg, unsigned n, const Params&
         // an incompressible chunk of a multi-chunk message: stored outright
         // (lz_core.h INCOMP_STORED)
         if (L.parser == P_STORED || (INCOMP_STORED && chunk_incomp && n > (unsigned)P.chunk) ||
-            (uint64_t)clen + 4 <= (opt_b < fix_b ? opt_b : fix_b)) {
+            chunk_stored(clen, opt_b < fix_b ? opt_b : fix_b, n > (unsigned)P.chunk)) {
             if (base == (unsigned)P.chunk) marker(base);   // chunk 1 carries a marker whatever its kind
             bw.put(0, 3);
             bw.align();
