@@ -824,6 +824,12 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
     // that finds the queue empty sends EXIT
     uint32_t msg = m;
     bool send_new = false, send_exit = false, exhausted = qctr == nullptr;
+#ifdef BPMD_PROF
+    // per message / task (prof build): lifetime from begin() to its END token,
+    // decoder iterations, and 4-byte stored-copy steps -> g_l3hprof[5-7]
+    unsigned long long tk_t0_ = 0;
+    uint32_t tk_it_ = 0, tk_sc_ = 0;
+#endif
     const uint32_t first_slots = s0 + gridDim.x * WG_MSGS;
     // the bit reader over payload bytes [p, p + n) (+ the pmd tail)
     auto open_view = [&](const uint8_t* p, uint32_t nn) {
@@ -848,6 +854,11 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
     };
     auto begin = [&](uint32_t mm) {
         msg = mm;
+#ifdef BPMD_PROF
+        tk_t0_ = __builtin_amdgcn_s_memtime();
+        tk_it_ = 0;
+        tk_sc_ = 0;
+#endif
         uint32_t byte0 = 0, bit0 = 0, kind = 0;
         bool skip = false;
         if (SEG) {
@@ -1277,6 +1288,9 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
             // COPY (inflate_stream.ipp:206-220): up to 4 bytes per iteration,
             // as a literal entry for the expander
             if (srem && room) {
+#ifdef BPMD_PROF
+                ++tk_sc_;
+#endif
                 refill();
                 const uint32_t k = srem < 4 ? srem : 4u;
                 elit = (uint32_t)bb;
@@ -1545,6 +1559,16 @@ __device__ __forceinline__ void decoder(uint8_t* T, bool valid, uint32_t m, cons
             head += adv ? 1u : 0u;
             lds_store((uint8_t*)lw(T, W_HEAD), head);
             fin = fin || (adv && endt);
+#ifdef BPMD_PROF
+            ++tk_it_;
+            if (adv && endt) {
+                // low 24 bits: the task (17 bits) and its result (7 bits)
+                const unsigned long long id = (msg & 0x1ffffu) | (((uint32_t)result & 0x7fu) << 17);
+                atomicMax(&g_l3hprof[5], ((__builtin_amdgcn_s_memtime() - tk_t0_) << 24) | id);
+                atomicMax(&g_l3hprof[6], ((unsigned long long)tk_it_ << 24) | id);
+                atomicAdd(&g_l3hprof[7], (unsigned long long)tk_sc_);
+            }
+#endif
             if (adv && ctl) {
                 if (send_new) begin(msg);
                 send_new = false;

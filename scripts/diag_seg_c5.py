@@ -59,6 +59,15 @@ def main():
     for i, nm in enumerate(NAMES):
         o, bv = rows["own"][i], rows["beast"][i]
         print(f"{nm:32s} {o:16d} {bv:16d} {bv / o if o else float('nan'):10.2f}")
+    # per-task records (prof build, g_l3hprof[5-7]): the longest task by
+    # lifetime and by decoder iterations (task index, its result), and the
+    # 4-byte stored-copy steps of all tasks
+    for name in ("own", "beast"):
+        r = rows[name]
+        t5, t6 = r[21], r[22]
+        print(f"{name}: longest task {t5 & 0x1ffff} (result {(t5 >> 17) & 0x7f}) {t5 >> 24} cycles; "
+              f"most iterations task {t6 & 0x1ffff} (result {(t6 >> 17) & 0x7f}) {t6 >> 24}; "
+              f"stored-copy steps {r[23]}")
 
 
 if __name__ == "__main__":
