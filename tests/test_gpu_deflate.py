@@ -111,6 +111,21 @@ def test_random_mixture():
         _check_model(msgs, pl, level)
 
 
+@pytest.mark.parametrize("level", [1, 6])
+def test_minimum_gain_chunk_choice_equals_model(level):
+    """lz::chunk_stored: chunks of long messages that save under 1/16 are stored,
+    one-chunk messages keep Beast's rule; the kernel makes the host model's
+    choice on data either side of the threshold (tests/test_model.py)."""
+    from tests.test_model import _slightly_compressible
+    msgs = []
+    for seed, frac in ((3, 1 / 16), (4, 1 / 8), (5, 1 / 4), (6, 1 / 32)):
+        d = _slightly_compressible(65536, seed, frac).tobytes()
+        msgs += [d, d[:4096], d[:9000]]
+    st, pl = _deflate(msgs, level=level)
+    _check_roundtrip(msgs, pl, st)
+    _check_model(msgs, pl, level)
+
+
 @pytest.mark.parametrize("level", [1, 6, 9])
 def test_size_tolerance_vs_beast(level):
     n = 2048

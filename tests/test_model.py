@@ -72,3 +72,36 @@ def test_runwise_code_length_coding_equals_serial_state_machine():
         buf = (ctypes.c_uint8 * n)(*lens)
         ok = L.dmodel_rle_check(buf, n, out1, out2, ctypes.byref(na), ctypes.byref(nb))
         assert ok == 1, (lens, na.value, nb.value)
+
+
+def _slightly_compressible(n, seed, frac):
+    # random bytes; a fraction of the 64-byte units copies 16-47 bytes from up
+    # to 1.5 KiB back (inside a chunk's 2 KiB history), like C5's binary kind
+    rng = np.random.default_rng(seed)
+    d = rng.integers(0, 256, n, dtype=np.uint8)
+    for p in range(64, n, 64):
+        if rng.random() < frac:
+            span = int(rng.integers(16, 48))
+            back = int(rng.integers(span, min(p, 1500) + 1))
+            d[p:p + span] = d[p - back:p - back + span]
+    return d
+
+
+def test_minimum_gain_for_chunks_of_long_messages():
+    """lz::chunk_stored (lz_core.h, BPMD_MIN_GAIN_SHIFT 4): a Huffman chunk of a
+    multi-chunk message must save 1/16 of its bytes, else it is stored; a
+    one-chunk message keeps Beast's rule (tr_flush_block,
+    deflate_stream.ipp:1478: any saving keeps the Huffman block)."""
+    data = _slightly_compressible(16384, 3, 1 / 16)
+    (multi,) = M.encode(data, [0], [16384], level=1)
+    st, out = O.pmd_inflate(multi, cap=16384)
+    assert st == 0 and out == data.tobytes()
+    assert len(multi) >= 16384   # every chunk saved < 256 bytes: all stored
+    single = [M.encode(data[i * 4096:(i + 1) * 4096], [0], [4096], level=1)[0] for i in range(4)]
+    assert sum(len(s) < 4096 for s in single) >= 2   # the same chunks alone: Huffman blocks
+    # chunks that save more than 1/16 keep their Huffman blocks
+    data = _slightly_compressible(16384, 3, 1 / 4)
+    (multi,) = M.encode(data, [0], [16384], level=1)
+    st, out = O.pmd_inflate(multi, cap=16384)
+    assert st == 0 and out == data.tobytes()
+    assert len(multi) < 16384 * 15 // 16 + 64
