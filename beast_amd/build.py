@@ -22,6 +22,18 @@ CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-W
             "-munsafe-fp-atomics"]
 
 
+# Machine scheduler per translation unit (LLVM AMDGPU -amdgpu-sched-strategy),
+# measured interleaved on one MI355X (profiles/r06v_ab_sched_strategy.log):
+# the lane decoder (issue-bound, dependent LDS lookups) gains from
+# iterative-ilp -- C2 189.3 -> 191.2 GiB/s, inflate_lane3_kernel 1.305 -> 1.290
+# ms, C5 own / Beast inflate +1.5 / +2 % -- and the deflate parse from max-ilp
+# -- C3 52.6 -> 54.1, C4 30.9 -> 31.4 GiB/s.  Same results bit for bit.
+SRC_FLAGS = {
+    "pmd_inflate_lane3.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
+    "pmd_deflate.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+}
+
+
 def _sources():
     return sorted(f for f in os.listdir(CSRC) if f.endswith(".hip"))
 
@@ -37,7 +49,7 @@ def _compile(src: str, hmt: float, bdir: str = BUILD, extra=()) -> str:
     s = os.path.join(CSRC, src)
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(s), hmt):
         return obj
-    cmd = [HIPCC, *CXXFLAGS, *extra, "-c", s, "-o", obj]
+    cmd = [HIPCC, *CXXFLAGS, *SRC_FLAGS.get(src, []), *extra, "-c", s, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
